@@ -1,0 +1,154 @@
+/*
+ * rti.h -- C ABI of the MI355X-native RTI reflectance fitter (PTM / HSH).
+ *
+ * Drop-in boundary for the per-pixel reflectance-fit hot path of
+ * bara96/Smartphone-based-RTI (reference @ v0).  The reference has no FFI of
+ * its own: the path sits behind plain Python calls in analysis.py.  Each entry
+ * point below names the reference code it replaces.  The Python package
+ * (smartphone-based-rti_amd/rti) binds these symbols with ctypes; INTEGRATION.md
+ * shows the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Functions named rti_fit_* / rti_relight*
+ *     take DEVICE pointers (hipMalloc'd or torch CUDA tensors) and enqueue
+ *     asynchronously on `stream` (a hipStream_t; NULL = default stream).  They
+ *     never allocate, free or synchronise, so they can be captured in a
+ *     hipGraph.  Functions named rti_design_* / rti_pinv / rti_basis_* are
+ *     host-only and take HOST pointers.
+ *   - Return value: RTI_OK (0) or an RTI_ERR_* status; rti_last_error()
+ *     returns a thread-local message for the most recent failure.
+ *   - Reentrant: no global mutable state besides the thread-local message.
+ *   - Intensity stacks are LIGHT-MAJOR: I[c][n][p] with pixel p = y*W + x
+ *     contiguous inside one light plane (strides in elements; 0 = dense).
+ *     The reference stacks pixel-major [y][x][n] (analysis.py:217-219); the
+ *     per-pixel "dirs" entry point accepts that layout.
+ */
+#ifndef RTI_H
+#define RTI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define RTI_OK              0
+#define RTI_ERR_BAD_ARG     1   /* null pointer, non-positive size, k/N mismatch, N < k */
+#define RTI_ERR_UNSUPPORTED 2   /* valid but unsupported combination (dtype/basis/layout) */
+#define RTI_ERR_HIP         3   /* HIP runtime error at launch */
+
+/* ---- bases ---- */
+#define RTI_BASIS_PTM6  0   /* (lu², lv², lu·lv, lu, lv, 1), analysis.py:285 */
+#define RTI_BASIS_HSH16 1   /* hemispherical harmonics l=0..3 (build-defined) */
+#define RTI_BASIS_HSH9  2   /* hemispherical harmonics l=0..2 */
+
+/* ---- element types ---- */
+#define RTI_F32 0
+#define RTI_U8  1
+#define RTI_I32 2
+#define RTI_F64 3
+
+/* ---- coefficient layouts ---- */
+#define RTI_COEF_PIXEL_MAJOR 0  /* coef[c][p][k] */
+#define RTI_COEF_PLANAR      1  /* coef[c][k][p] */
+
+/* ---- relight output layouts ---- */
+#define RTI_OUT_EVAL_MAJOR  0   /* out[e][p]: one image per light (prepare_images_data order) */
+#define RTI_OUT_PIXEL_MAJOR 1   /* out[p][e]: interpolate_intensities order [y][x][ly][lx] */
+
+/* ---- shared-fit kernel selection ---- */
+#define RTI_KERNEL_AUTO 0
+#define RTI_KERNEL_VALU 1   /* pinv in SGPRs, fp32 FMA stream */
+#define RTI_KERNEL_MFMA 2   /* v_mfma_f32_16x16x4_f32, pinv staged in LDS */
+#define RTI_KERNEL_NONTEMPORAL 0x100  /* OR-able flag: non-temporal loads of the intensity stream */
+
+typedef void* rti_stream_t; /* hipStream_t */
+
+/* ---- library info ---- */
+int         rti_version(void);                 /* 10000*major + 100*minor + patch */
+const char* rti_status_string(int status);
+const char* rti_last_error(void);
+int         rti_basis_terms(int basis);        /* k for a basis, or -1 */
+int         rti_device_count(void);            /* hipGetDeviceCount, 0 on failure */
+
+/* ---- host: basis / design matrix / pseudo-inverse ----------------------------------
+ * rti_design_matrix replaces the design-row loop of _interpolate_PTM
+ * (analysis.py:280-291): A[n][k] in fp64 with PTM monomials formed in fp32 from
+ * fp32 (lu, lv), as the reference does.
+ * rti_pinv replaces the SVD solve (analysis.py:293-298) for a SHARED light set:
+ * pinv[k][n] = V Σ⁻¹ Uᵀ by one-sided Jacobi SVD in fp64.  rcond < 0 keeps the
+ * reference's semantics (no threshold: a zero singular value gives inf/NaN);
+ * rcond >= 0 zeroes σ <= rcond·σ_max.  Returns RTI_ERR_BAD_ARG when n < k
+ * (the reference raises ValueError at analysis.py:298).
+ * rti_basis_eval evaluates the basis at E host (lu, lv) pairs (fp64 inputs). */
+int rti_design_matrix(int basis, const float* lu, const float* lv, int n, double* A);
+int rti_pinv(int basis, const float* lu, const float* lv, int n, double rcond, double* pinv);
+int rti_basis_eval(int basis, const double* lu, const double* lv, int E, double* out);
+
+/* ---- device: shared-direction fit (the north_star hot path) ------------------------
+ * Replaces interpolate_intensities' per-pixel loop + _interpolate_PTM's solve
+ * (analysis.py:321-363, :293-298) when every pixel sees the same light set:
+ *   coef[c][p][i] = Σ_n pinv[i][n] · I[c][n][p]
+ * pinv: device fp32 [k][N].  I: device, dtype in_dtype (F32, U8 or I32),
+ * element (c,n,p) at c*channel_stride + n*light_stride + p
+ * (light_stride 0 = P, channel_stride 0 = N*light_stride).
+ * coef: device fp32, layout coef_layout, channel stride coef_channel_stride
+ * (0 = P*k).  k must equal rti_basis_terms(basis) for some basis, or any
+ * 1 <= k <= 16 with kernel = RTI_KERNEL_MFMA. */
+int rti_fit_shared(const float* pinv, int k, int N,
+                   const void* I, int in_dtype, int64_t P, int C,
+                   int64_t light_stride, int64_t channel_stride,
+                   float* coef, int coef_layout, int64_t coef_channel_stride,
+                   int kernel, rti_stream_t stream);
+
+/* ---- device: per-pixel PTM fit, light vectors generated in-kernel ------------------
+ * Fuses compute_intensities' light vectors (analysis.py:221-231) into the
+ * per-pixel PTM solve (analysis.py:280-298): for pixel (x, y) of an H×W stack
+ * and camera n, l = (cam_n − (x0+x, y0+y, 0)) / ‖·‖ (fp64, rounded to fp32 as
+ * the reference stores lx/ly in float32), then the 6×6 normal equations are
+ * accumulated and solved in fp64 (Cholesky).  cams: device fp64 [N][3].
+ * I: device light-major [N][light_stride] (0 = H*W), dtype F32/U8/I32.
+ * coef: device, coef_dtype F32 or F64, layout coef_layout.
+ * rcond < 0: reference semantics (exactly singular → NaN coefficients);
+ * rcond >= 0: pivots <= rcond²·max_pivot are treated as singular → NaN. */
+int rti_fit_perpixel_cam(const double* cams, int N,
+                         const void* I, int in_dtype, int H, int W, int64_t light_stride,
+                         double x0, double y0, double rcond,
+                         void* coef, int coef_dtype, int coef_layout, rti_stream_t stream);
+
+/* ---- device: per-pixel PTM fit from explicit per-pixel light vectors ---------------
+ * The exact input of interpolate_intensities (analysis.py:321-363): lu, lv
+ * (fp32) and I (F32/U8/I32), each PIXEL-major [P][N] as compute_intensities
+ * returns them (analysis.py:217-219).  Same solve and output as above. */
+int rti_fit_perpixel_dirs(const float* lu, const float* lv, const void* I, int in_dtype,
+                          int N, int64_t P, double rcond,
+                          void* coef, int coef_dtype, int coef_layout, rti_stream_t stream);
+
+/* ---- device: light vectors ---------------------------------------------------------
+ * The light-vector half of compute_intensities (analysis.py:221-231) for an
+ * H×W ROI and N cameras: lu[p][n], lv[p][n] (fp32, pixel-major, p = y*W + x),
+ * l = (cam_n − (x0+x, y0+y, 0)) / ‖·‖ in fp64 rounded to fp32. */
+int rti_light_dirs(const double* cams, int N, int H, int W, double x0, double y0,
+                   float* lu, float* lv, rti_stream_t stream);
+
+/* ---- device: relight evaluator -----------------------------------------------------
+ * Replaces _interpolate_PTM's grid evaluation (analysis.py:300-315), the
+ * prepare_images_data transpose/truncation (analysis.py:375-411) and the
+ * relighting_event lookup + clip (interactive_relighting.py:25-36):
+ *   out[e][p] (or out[p][e]) = Σ_i coef[p][i] · b_i(lu_e, lv_e)
+ * coef: device, coef_dtype F32 or F64 (arithmetic is done in that type; the
+ * F64 PTM path sums the six terms left to right without contraction, exactly
+ * as analysis.py:307-312).  luv: device fp64 [E][2] (lu, lv).
+ * out_dtype: F32 / F64 value; I32 = C truncation toward zero, NaN/overflow →
+ * INT32_MIN (the int32 assignment of analysis.py:407 on x86); U8 = the I32
+ * value clipped to [0, 255] (interactive_relighting.py:35-36). */
+int rti_relight(const void* coef, int coef_dtype, int basis, int64_t P, int coef_layout,
+                const double* luv, int E,
+                void* out, int out_dtype, int out_layout, rti_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTI_H */

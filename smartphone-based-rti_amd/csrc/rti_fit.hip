@@ -1,0 +1,365 @@
+// rti_fit.hip -- shared-direction PTM/HSH fit on gfx950 (MI355X).
+//
+// Replaces the per-pixel loop of interpolate_intensities + the SVD solve of
+// _interpolate_PTM (analysis.py:321-363, :293-298) for a shared light set:
+//     coef[c][p][i] = Σ_n pinv[i][n] · I[c][n][p]
+// i.e. the k×N pseudo-inverse applied to the light-major intensity stack.
+//
+// The contraction is HBM-bound (arithmetic intensity 1.5 flop/B for PTM-6,
+// 4 flop/B for HSH-16, ridge ≈20 flop/B), so both kernels are built around
+// the intensity stream: every byte of I is read exactly once, with 16-byte
+// coalesced loads, and the k×N operator never touches HBM after the first
+// wave reads it.
+//
+//  * fit_shared_valu<K>: one lane owns VEC adjacent pixels (16 B of one light
+//    plane per load), the k×N pseudo-inverse is wave-uniform and is read with
+//    scalar loads into SGPRs, the contraction is K·VEC fp32 FMAs per load.
+//  * fit_shared_mfma: the pseudo-inverse is staged once per workgroup in LDS
+//    as [N][16] and fed as the A operand of v_mfma_f32_16x16x4_f32; the
+//    intensity stream is the B operand.  A lane's 16-B load (4 pixels of one
+//    light) supplies B for four 16-pixel MFMA tiles (pixel j of tile c is
+//    p0 + 4j + c), so the four accumulators are independent and the load is
+//    still 256 contiguous bytes per 16 lanes.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "rti_basis.h"
+#include "rti_internal.h"
+
+namespace rti {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// ---- VEC adjacent pixels of one light plane -> fp32 registers ------------------------
+template <typename T, int VEC, bool NT>
+__device__ __forceinline__ void load_px(const T* __restrict__ p, float (&x)[VEC]) {
+  if constexpr (VEC == 1) {
+    x[0] = (float)(NT ? __builtin_nontemporal_load(p) : *p);
+  } else {
+    typedef T vec_t __attribute__((ext_vector_type(VEC)));
+    const vec_t* vp = reinterpret_cast<const vec_t*>(p);
+    vec_t v = NT ? __builtin_nontemporal_load(vp) : *vp;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) x[i] = (float)v[i];
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void store_f32(float* __restrict__ dst, const float (&v)[N]) {
+  if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      floatx4 t = {v[i], v[i + 1], v[i + 2], v[i + 3]};
+      *reinterpret_cast<floatx4*>(dst + i) = t;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) dst[i] = v[i];
+  }
+}
+
+// ---- VALU stream kernel ---------------------------------------------------------------
+template <int K, int VEC, typename T, int LAYOUT, bool NT>
+__global__ void __launch_bounds__(256)
+fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P,
+                int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
+  if (p0 >= P) return;
+  const T* __restrict__ src = I + (int64_t)blockIdx.y * cstride + p0;
+
+  float acc[K][VEC];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[k][v] = 0.f;
+
+  constexpr int U = (VEC >= 16) ? 4 : 8;  // loads in flight per lane
+  int n = 0;
+  for (; n + U <= N; n += U) {
+    float x[U][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_px<T, VEC, NT>(src + (int64_t)(n + u) * lstride, x[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float w = pinv[k * N + n + u];  // wave-uniform -> s_load
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[k][v] = fmaf(w, x[u][v], acc[k][v]);
+      }
+  }
+  for (; n < N; ++n) {
+    float x[VEC];
+    load_px<T, VEC, NT>(src + (int64_t)n * lstride, x);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float w = pinv[k * N + n];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[k][v] = fmaf(w, x[v], acc[k][v]);
+    }
+  }
+
+  float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
+  if constexpr (LAYOUT == RTI_COEF_PLANAR) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) store_f32<VEC>(dst + (int64_t)k * P + p0, acc[k]);
+  } else {
+    float o[VEC * K];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+      for (int k = 0; k < K; ++k) o[v * K + k] = acc[k][v];
+    store_f32<VEC * K>(dst + p0 * K, o);
+  }
+}
+
+// ---- MFMA kernel (k <= 16) ------------------------------------------------------------
+// Block = 4 waves; wave w owns the 64 pixels [p0, p0+64) with
+// p0 = (4·blockIdx.x + w)·64.  Lane l: q = l & 15 (MFMA column), r = l >> 4
+// (MFMA k-row = light n0 + r).  D[i][j] of accumulator c is coefficient i of
+// pixel p0 + 4j + c; lane l holds rows 4r..4r+3 of column q.
+template <typename T, int LAYOUT, bool NT>
+__global__ void __launch_bounds__(256)
+fit_shared_mfma(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P,
+                int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  extern __shared__ __attribute__((aligned(16))) float lds_pinv[];  // [Npad][16]
+  const int Npad = (N + 3) & ~3;
+  for (int idx = threadIdx.x; idx < Npad * 16; idx += 256) {
+    const int n = idx >> 4, i = idx & 15;
+    lds_pinv[idx] = (i < k && n < N) ? pinv[i * N + n] : 0.f;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (p0 >= P) return;
+  const int q = lane & 15, r = lane >> 4;
+  const int64_t px = p0 + 4 * q;
+  const bool lane_ok = px < P;                 // P % 4 == 0 is guaranteed by the launcher
+  const T* __restrict__ src = I + (int64_t)blockIdx.y * cstride + (lane_ok ? px : P - 4);
+
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+  const float* a_col = lds_pinv + r * 16 + q;
+  constexpr int S = 8;  // k-steps (4 lights each) whose loads are in flight together
+  int n0 = 0;
+  for (; n0 + 4 * S <= Npad; n0 += 4 * S) {
+    float x[S][4];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      int n = n0 + 4 * s + r;
+      n = n < N ? n : N - 1;  // the padded rows of A are zero
+      load_px<T, 4, NT>(src + (int64_t)n * lstride, x[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const float a = a_col[(n0 + 4 * s) * 16];
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[s][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[s][1], acc1, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[s][2], acc2, 0, 0, 0);
+      acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[s][3], acc3, 0, 0, 0);
+    }
+  }
+  for (; n0 < Npad; n0 += 4) {
+    int n = n0 + r;
+    n = n < N ? n : N - 1;
+    float x[4];
+    load_px<T, 4, NT>(src + (int64_t)n * lstride, x);
+    const float a = a_col[n0 * 16];
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[0], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[1], acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[2], acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[3], acc3, 0, 0, 0);
+  }
+  if (!lane_ok) return;
+
+  float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
+  if constexpr (LAYOUT == RTI_COEF_PLANAR) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int i = 4 * r + rr;
+      if (i < k) {
+        floatx4 t = {acc0[rr], acc1[rr], acc2[rr], acc3[rr]};
+        *reinterpret_cast<floatx4*>(dst + (int64_t)i * P + px) = t;
+      }
+    }
+  } else {
+    if (k == 16) {
+      *reinterpret_cast<floatx4*>(dst + (px + 0) * 16 + 4 * r) = acc0;
+      *reinterpret_cast<floatx4*>(dst + (px + 1) * 16 + 4 * r) = acc1;
+      *reinterpret_cast<floatx4*>(dst + (px + 2) * 16 + 4 * r) = acc2;
+      *reinterpret_cast<floatx4*>(dst + (px + 3) * 16 + 4 * r) = acc3;
+    } else {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = 4 * r + rr;
+        if (i < k) {
+          dst[(px + 0) * k + i] = acc0[rr];
+          dst[(px + 1) * k + i] = acc1[rr];
+          dst[(px + 2) * k + i] = acc2[rr];
+          dst[(px + 3) * k + i] = acc3[rr];
+        }
+      }
+    }
+  }
+}
+
+struct FitArgs {
+  const float* pinv;
+  int k, N;
+  const void* I;
+  int64_t P;
+  int C;
+  int64_t lstride, cstride;
+  float* coef;
+  int layout;
+  int64_t ocstride;
+  bool nt;
+  hipStream_t stream;
+};
+
+template <int K, int VEC, typename T, int LAYOUT, bool NT>
+void launch_valu_t(const FitArgs& a) {
+  const int64_t groups = (a.P + VEC - 1) / VEC;
+  dim3 grid(grid_1d(groups, 256), a.C);
+  hipLaunchKernelGGL((fit_shared_valu<K, VEC, T, LAYOUT, NT>), grid, dim3(256), 0, a.stream, a.pinv, a.N,
+                     static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride);
+}
+
+template <int K, int VEC, typename T>
+void launch_valu_l(const FitArgs& a) {
+  if (a.layout == RTI_COEF_PLANAR)
+    a.nt ? launch_valu_t<K, VEC, T, RTI_COEF_PLANAR, true>(a) : launch_valu_t<K, VEC, T, RTI_COEF_PLANAR, false>(a);
+  else
+    a.nt ? launch_valu_t<K, VEC, T, RTI_COEF_PIXEL_MAJOR, true>(a)
+         : launch_valu_t<K, VEC, T, RTI_COEF_PIXEL_MAJOR, false>(a);
+}
+
+template <int K, typename T>
+void launch_valu_v(const FitArgs& a, bool vec_ok) {
+  constexpr int VEC = std::is_same<T, uint8_t>::value ? (K <= 6 ? 16 : 4) : 4;
+  if (vec_ok)
+    launch_valu_l<K, VEC, T>(a);
+  else
+    launch_valu_l<K, 1, T>(a);
+}
+
+template <typename T>
+void launch_valu(const FitArgs& a, bool vec_ok) {
+  switch (a.k) {
+    case 6: launch_valu_v<6, T>(a, vec_ok); break;
+    case 9: launch_valu_v<9, T>(a, vec_ok); break;
+    default: launch_valu_v<16, T>(a, vec_ok); break;
+  }
+}
+
+template <typename T>
+void launch_mfma(const FitArgs& a) {
+  const int Npad = (a.N + 3) & ~3;
+  const size_t lds = (size_t)Npad * 16 * sizeof(float);
+  dim3 grid(grid_1d(a.P, 256), a.C);
+  if (a.layout == RTI_COEF_PLANAR) {
+    if (a.nt)
+      hipLaunchKernelGGL((fit_shared_mfma<T, RTI_COEF_PLANAR, true>), grid, dim3(256), lds, a.stream, a.pinv, a.k,
+                         a.N, static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride);
+    else
+      hipLaunchKernelGGL((fit_shared_mfma<T, RTI_COEF_PLANAR, false>), grid, dim3(256), lds, a.stream, a.pinv, a.k,
+                         a.N, static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride);
+  } else {
+    if (a.nt)
+      hipLaunchKernelGGL((fit_shared_mfma<T, RTI_COEF_PIXEL_MAJOR, true>), grid, dim3(256), lds, a.stream, a.pinv,
+                         a.k, a.N, static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride);
+    else
+      hipLaunchKernelGGL((fit_shared_mfma<T, RTI_COEF_PIXEL_MAJOR, false>), grid, dim3(256), lds, a.stream, a.pinv,
+                         a.k, a.N, static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride);
+  }
+}
+
+size_t dtype_size(int dt) {
+  switch (dt) {
+    case RTI_F32: return 4;
+    case RTI_I32: return 4;
+    case RTI_U8: return 1;
+    case RTI_F64: return 8;
+    default: return 0;
+  }
+}
+
+}  // namespace
+}  // namespace rti
+
+using namespace rti;
+
+extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
+                              int64_t light_stride, int64_t channel_stride, float* coef, int coef_layout,
+                              int64_t coef_channel_stride, int kernel, rti_stream_t stream) {
+  if (!pinv || !I || !coef) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: null pointer");
+  if (N <= 0 || P <= 0 || C <= 0 || C > 65535) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: bad N/P/C");
+  if (k < 1 || k > 16) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: k=%d outside 1..16", k);
+  if (N < k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: N=%d < k=%d", N, k);
+  if (in_dtype != RTI_F32 && in_dtype != RTI_U8 && in_dtype != RTI_I32)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: input dtype %d", in_dtype);
+  if (coef_layout != RTI_COEF_PIXEL_MAJOR && coef_layout != RTI_COEF_PLANAR)
+    return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: coef layout %d", coef_layout);
+  FitArgs a;
+  a.pinv = pinv;
+  a.k = k;
+  a.N = N;
+  a.I = I;
+  a.P = P;
+  a.C = C;
+  a.lstride = light_stride ? light_stride : P;
+  a.cstride = channel_stride ? channel_stride : (int64_t)N * a.lstride;
+  a.coef = coef;
+  a.layout = coef_layout;
+  a.ocstride = coef_channel_stride ? coef_channel_stride : P * k;
+  a.nt = (kernel & RTI_KERNEL_NONTEMPORAL) != 0;
+  a.stream = (hipStream_t)stream;
+  if (a.lstride < P) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: light_stride < P");
+  if (C > 1 && a.cstride < (int64_t)N * a.lstride) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: channel_stride");
+  if (C > 1 && a.ocstride < P * k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: coef_channel_stride");
+
+  const size_t es = dtype_size(in_dtype);
+  auto vec_ok_for = [&](int vec) {
+    const bool in_ok = P % vec == 0 && a.lstride % vec == 0 && a.cstride % vec == 0 && aligned_to(I, vec * es);
+    const bool out_ok = aligned_to(coef, 16) && (a.ocstride % 4 == 0) &&
+                        (coef_layout == RTI_COEF_PLANAR ? P % 4 == 0 : (vec * k) % 4 == 0);
+    return in_ok && out_ok;
+  };
+  const int sel = kernel & 0xff;
+  const bool valu_k = (k == 6 || k == 9 || k == 16);
+  bool use_mfma;
+  if (sel == RTI_KERNEL_MFMA)
+    use_mfma = true;
+  else if (sel == RTI_KERNEL_VALU)
+    use_mfma = false;
+  else
+    use_mfma = !valu_k || k == 16;
+  const bool mfma_ok = N <= 2048 && P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 &&
+                       aligned_to(I, 4 * es) && aligned_to(coef, 16) && a.ocstride % 4 == 0;
+  if (use_mfma && !mfma_ok) {
+    if (sel == RTI_KERNEL_MFMA && !valu_k)
+      return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: MFMA path needs N<=2048 and 4-pixel alignment");
+    use_mfma = false;
+  }
+  if (!use_mfma && !valu_k) return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: VALU path supports k in {6,9,16}");
+
+  if (use_mfma) {
+    switch (in_dtype) {
+      case RTI_F32: launch_mfma<float>(a); break;
+      case RTI_I32: launch_mfma<int32_t>(a); break;
+      default: launch_mfma<uint8_t>(a); break;
+    }
+  } else {
+    const int vec = in_dtype == RTI_U8 ? (k <= 6 ? 16 : 4) : 4;
+    const bool vok = vec_ok_for(vec);
+    switch (in_dtype) {
+      case RTI_F32: launch_valu<float>(a, vok); break;
+      case RTI_I32: launch_valu<int32_t>(a, vok); break;
+      default: launch_valu<uint8_t>(a, vok); break;
+    }
+  }
+  return check_launch("rti_fit_shared");
+}

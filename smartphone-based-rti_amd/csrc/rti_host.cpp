@@ -1,0 +1,183 @@
+// rti_host.cpp -- host half of the C ABI: status strings, design matrices and
+// the shared pseudo-inverse (fp64 one-sided Jacobi SVD).
+//
+// rti_design_matrix restates the design-row loop of _interpolate_PTM
+// (analysis.py:280-291); rti_pinv restates its SVD solve (analysis.py:293-298)
+// as an explicit k×N operator so a single device contraction can apply it to
+// every pixel.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "rti_basis.h"
+#include "rti_internal.h"
+
+namespace rti {
+
+thread_local char g_last_error[512] = "";
+
+int fail(int status, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+  return status;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(RTI_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return RTI_OK;
+}
+
+// PTM row exactly as analysis.py:284-285: monomials of float32 lu/lv formed in
+// float32, then widened (np.array of the tuple is float64).  The reference's
+// `lu ** 2` is C powf on a NumPy float32 scalar; x*x is its correctly rounded
+// value (they can differ by 1 ulp, far inside the fp32 parity tolerance).
+static void ptm_row(float lu, float lv, double* row) {
+  row[0] = (double)(lu * lu);
+  row[1] = (double)(lv * lv);
+  row[2] = (double)(lu * lv);
+  row[3] = (double)lu;
+  row[4] = (double)lv;
+  row[5] = 1.0;
+}
+
+static void design_row(int basis, float lu, float lv, double* row) {
+  if (basis == RTI_BASIS_PTM6)
+    ptm_row(lu, lv, row);
+  else
+    hsh_eval<double>((double)lu, (double)lv, basis_terms(basis), row);
+}
+
+// One-sided (Hestenes) Jacobi SVD of A[n][k] (row-major, n >= k) and
+// pinv[k][n] = V Σ⁻¹ Uᵀ = Σ_m v_m (A v_m)ᵀ / σ_m².
+static void jacobi_pinv(const double* A, int n, int k, double rcond, double* pinv) {
+  std::vector<double> U(A, A + (size_t)n * k);  // column j = U[i*k + j]; becomes U·Σ
+  std::vector<double> V((size_t)k * k, 0.0);
+  for (int j = 0; j < k; ++j) V[(size_t)j * k + j] = 1.0;
+  const double tol = 1e-15;
+  for (int sweep = 0; sweep < 100; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < k - 1; ++p) {
+      for (int q = p + 1; q < k; ++q) {
+        double alpha = 0, beta = 0, gamma = 0;
+        for (int i = 0; i < n; ++i) {
+          const double up = U[(size_t)i * k + p], uq = U[(size_t)i * k + q];
+          alpha += up * up;
+          beta += uq * uq;
+          gamma += up * uq;
+        }
+        if (gamma == 0.0 || alpha == 0.0 || beta == 0.0) continue;
+        const double rel = std::fabs(gamma) / std::sqrt(alpha * beta);
+        if (rel <= tol) continue;
+        off = std::fmax(off, rel);
+        const double zeta = (beta - alpha) / (2.0 * gamma);
+        const double t = std::copysign(1.0, zeta) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / std::sqrt(1.0 + t * t), s = c * t;
+        for (int i = 0; i < n; ++i) {
+          double& up = U[(size_t)i * k + p];
+          double& uq = U[(size_t)i * k + q];
+          const double a = up, b = uq;
+          up = c * a - s * b;
+          uq = s * a + c * b;
+        }
+        for (int i = 0; i < k; ++i) {
+          double& vp = V[(size_t)i * k + p];
+          double& vq = V[(size_t)i * k + q];
+          const double a = vp, b = vq;
+          vp = c * a - s * b;
+          vq = s * a + c * b;
+        }
+      }
+    }
+    if (off <= tol) break;
+  }
+  std::vector<double> sig2(k);
+  double smax = 0.0;
+  for (int m = 0; m < k; ++m) {
+    double s2 = 0;
+    for (int i = 0; i < n; ++i) s2 += U[(size_t)i * k + m] * U[(size_t)i * k + m];
+    sig2[m] = s2;
+    smax = std::fmax(smax, std::sqrt(s2));
+  }
+  std::vector<double> inv2(k);
+  for (int m = 0; m < k; ++m) {
+    const double sm = std::sqrt(sig2[m]);
+    if (rcond >= 0.0 && !(sm > rcond * smax))
+      inv2[m] = 0.0;  // truncated
+    else
+      inv2[m] = 1.0 / sig2[m];  // reference semantics: σ = 0 -> inf -> NaN entries
+  }
+  for (int j = 0; j < k; ++j)
+    for (int i = 0; i < n; ++i) {
+      double acc = 0.0;
+      for (int m = 0; m < k; ++m) {
+        if (inv2[m] == 0.0) continue;
+        acc += V[(size_t)j * k + m] * (U[(size_t)i * k + m] * inv2[m]);
+      }
+      pinv[(size_t)j * n + i] = acc;
+    }
+}
+
+}  // namespace rti
+
+using namespace rti;
+
+extern "C" {
+
+int rti_version(void) { return 100; /* 0.1.0 */ }
+
+const char* rti_status_string(int status) {
+  switch (status) {
+    case RTI_OK: return "ok";
+    case RTI_ERR_BAD_ARG: return "bad argument";
+    case RTI_ERR_UNSUPPORTED: return "unsupported";
+    case RTI_ERR_HIP: return "hip error";
+    default: return "unknown status";
+  }
+}
+
+const char* rti_last_error(void) { return g_last_error; }
+
+int rti_basis_terms(int basis) { return basis_terms(basis); }
+
+int rti_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int rti_design_matrix(int basis, const float* lu, const float* lv, int n, double* A) {
+  const int k = basis_terms(basis);
+  if (k < 0) return fail(RTI_ERR_BAD_ARG, "rti_design_matrix: unknown basis %d", basis);
+  if (!lu || !lv || !A || n <= 0) return fail(RTI_ERR_BAD_ARG, "rti_design_matrix: null pointer or n <= 0");
+  for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], A + (size_t)i * k);
+  return RTI_OK;
+}
+
+int rti_pinv(int basis, const float* lu, const float* lv, int n, double rcond, double* pinv) {
+  const int k = basis_terms(basis);
+  if (k < 0) return fail(RTI_ERR_BAD_ARG, "rti_pinv: unknown basis %d", basis);
+  if (!lu || !lv || !pinv || n <= 0) return fail(RTI_ERR_BAD_ARG, "rti_pinv: null pointer or n <= 0");
+  if (n < k)
+    return fail(RTI_ERR_BAD_ARG, "rti_pinv: %d lights < %d basis terms (shapes not aligned, analysis.py:298)", n, k);
+  std::vector<double> A((size_t)n * k);
+  for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], A.data() + (size_t)i * k);
+  jacobi_pinv(A.data(), n, k, rcond, pinv);
+  return RTI_OK;
+}
+
+int rti_basis_eval(int basis, const double* lu, const double* lv, int E, double* out) {
+  const int k = basis_terms(basis);
+  if (k < 0) return fail(RTI_ERR_BAD_ARG, "rti_basis_eval: unknown basis %d", basis);
+  if (!lu || !lv || !out || E <= 0) return fail(RTI_ERR_BAD_ARG, "rti_basis_eval: null pointer or E <= 0");
+  for (int e = 0; e < E; ++e) basis_eval<double>(basis, lu[e], lv[e], out + (size_t)e * k);
+  return RTI_OK;
+}
+
+}  // extern "C"

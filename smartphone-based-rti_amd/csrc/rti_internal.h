@@ -1,0 +1,22 @@
+// rti_internal.h -- helpers shared by the C-ABI translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+
+#include "../../include/rti.h"
+
+namespace rti {
+
+// Records a thread-local message (rti_last_error) and returns `status`.
+int fail(int status, const char* fmt, ...);
+// hipGetLastError after a launch -> RTI_OK or RTI_ERR_HIP.
+int check_launch(const char* what);
+
+inline bool aligned_to(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
+
+inline unsigned grid_1d(int64_t items, int per_block) { return (unsigned)((items + per_block - 1) / per_block); }
+
+}  // namespace rti

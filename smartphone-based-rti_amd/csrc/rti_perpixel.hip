@@ -1,0 +1,289 @@
+// rti_perpixel.hip -- reference-faithful per-pixel PTM fit on gfx950.
+//
+// In the reference every pixel has its OWN light list: compute_intensities
+// (analysis.py:221-232) gives pixel (x, y) and camera i the direction
+// l = (cam_i − (x, y, 0)) / ‖cam_i − (x, y, 0)‖, kept as float32 lx/ly, and
+// _interpolate_PTM (analysis.py:280-298) solves that pixel's N×6 system by SVD
+// without rcond.  Here one lane owns one pixel: it forms the PTM row in fp32
+// (as the reference's float32 monomials), accumulates the 6×6 normal
+// equations AᵀA, Aᵀb in fp64 and solves them by Cholesky in fp64.  For a
+// full-rank A that is the same least-squares solution the SVD returns (the
+// fp64 normal equations lose cond(A)²·1e-16, far below the 1e-4 parity
+// tolerance for cond(A) < 1e3); a rank-deficient A gives NaN coefficients, as
+// the reference's division by a zero singular value does.
+//
+//  * fit_perpixel_cam : directions generated in-kernel from cams[N][3]
+//    (light-major, coalesced intensity planes; no lx/ly traffic at all).
+//  * fit_perpixel_dirs: explicit pixel-major lx/ly/I [P][N], exactly the
+//    arrays interpolate_intensities receives (analysis.py:341-354).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rti_basis.h"
+#include "rti_internal.h"
+
+namespace rti {
+namespace {
+
+template <typename T>
+__device__ __forceinline__ double ld_d(const T* p) {
+  return (double)*p;
+}
+
+// Packed upper triangle of the symmetric 6×6 normal matrix.
+constexpr int tri(int i, int j) { return i <= j ? i * 6 - i * (i - 1) / 2 + (j - i) : tri(j, i); }
+
+struct Normal6 {
+  double m[21];
+  double b[6];
+};
+
+__device__ __forceinline__ void ne_zero(Normal6& ne) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) ne.m[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) ne.b[i] = 0.0;
+}
+
+// Row (lu², lv², lu·lv, lu, lv, 1.) with fp32 monomials (analysis.py:284-285).
+__device__ __forceinline__ void ne_add(Normal6& ne, float lu, float lv, double L) {
+  const double r[6] = {(double)(lu * lu), (double)(lv * lv), (double)(lu * lv), (double)lu, (double)lv, 1.0};
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int j = i; j < 6; ++j) ne.m[tri(i, j)] = fma(r[i], r[j], ne.m[tri(i, j)]);
+    ne.b[i] = fma(r[i], L, ne.b[i]);
+  }
+}
+
+// Cholesky solve of (AᵀA) a = Aᵀb.  rcond < 0: singular only at a non-positive
+// pivot (reference semantics); rcond >= 0: pivots <= rcond²·max(diag) count
+// as singular.  Singular -> all-NaN coefficients.
+__device__ __forceinline__ void ne_solve(const Normal6& ne, double rcond, double (&a)[6]) {
+  double L[6][6];
+  double dmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) dmax = fmax(dmax, ne.m[tri(i, i)]);
+  const double thr = rcond < 0.0 ? 0.0 : rcond * rcond * dmax;
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double d = ne.m[tri(j, j)];
+#pragma unroll
+    for (int p = 0; p < j; ++p) d -= L[j][p] * L[j][p];
+    ok = ok && (d > thr);
+    const double ljj = sqrt(d > 0.0 ? d : 1.0);
+    L[j][j] = ljj;
+    const double inv = 1.0 / ljj;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double s = ne.m[tri(i, j)];
+#pragma unroll
+      for (int p = 0; p < j; ++p) s -= L[i][p] * L[j][p];
+      L[i][j] = s * inv;
+    }
+  }
+  double y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double s = ne.b[i];
+#pragma unroll
+    for (int p = 0; p < i; ++p) s -= L[i][p] * y[p];
+    y[i] = s / L[i][i];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+#pragma unroll
+    for (int p = i + 1; p < 6; ++p) s -= L[p][i] * a[p];
+    a[i] = s / L[i][i];
+  }
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a[i] = __builtin_nan("");
+  }
+}
+
+template <typename TC, int LAYOUT>
+__device__ __forceinline__ void store_coef(TC* __restrict__ coef, int64_t P, int64_t p, const double (&a)[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if constexpr (LAYOUT == RTI_COEF_PLANAR)
+      coef[(int64_t)i * P + p] = (TC)a[i];
+    else
+      coef[p * 6 + i] = (TC)a[i];
+  }
+}
+
+template <typename T, typename TC, int LAYOUT>
+__global__ void __launch_bounds__(256)
+fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
+                 double x0, double y0, double rcond, TC* __restrict__ coef) {
+  const int64_t P = (int64_t)H * W;
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const double px = x0 + (double)(p % W);
+  const double py = y0 + (double)(p / W);
+  Normal6 ne;
+  ne_zero(ne);
+  const T* __restrict__ src = I + p;
+#pragma unroll 4
+  for (int n = 0; n < N; ++n) {
+    const double dx = cams[3 * n + 0] - px;  // cams: wave-uniform -> scalar loads
+    const double dy = cams[3 * n + 1] - py;
+    const double dz = cams[3 * n + 2];
+    const double nrm = sqrt(dx * dx + dy * dy + dz * dz);
+    const float lu = (float)(dx / nrm);  // float32 lx/ly (analysis.py:217-218, 230-231)
+    const float lv = (float)(dy / nrm);
+    ne_add(ne, lu, lv, ld_d(src + (int64_t)n * lstride));
+  }
+  double a[6];
+  ne_solve(ne, rcond, a);
+  store_coef<TC, LAYOUT>(coef, P, p, a);
+}
+
+template <typename T, typename TC, int LAYOUT>
+__global__ void __launch_bounds__(256)
+fit_perpixel_dirs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N,
+                  int64_t P, double rcond, TC* __restrict__ coef) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const int64_t base = p * N;
+  Normal6 ne;
+  ne_zero(ne);
+#pragma unroll 4
+  for (int n = 0; n < N; ++n) ne_add(ne, lu[base + n], lv[base + n], ld_d(I + base + n));
+  double a[6];
+  ne_solve(ne, rcond, a);
+  store_coef<TC, LAYOUT>(coef, P, p, a);
+}
+
+// compute_intensities' light vectors (analysis.py:225-231); lane = (pixel, camera),
+// camera fastest so the pixel-major [P][N] stores are contiguous.
+__global__ void __launch_bounds__(256)
+light_dirs(const double* __restrict__ cams, int N, int W, int64_t total, double x0, double y0,
+           float* __restrict__ lu, float* __restrict__ lv) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int n = (int)(i % N);
+  const int64_t p = i / N;
+  const double dx = cams[3 * n + 0] - (x0 + (double)(p % W));
+  const double dy = cams[3 * n + 1] - (y0 + (double)(p / W));
+  const double dz = cams[3 * n + 2];
+  const double nrm = sqrt(dx * dx + dy * dy + dz * dz);
+  lu[i] = (float)(dx / nrm);
+  lv[i] = (float)(dy / nrm);
+}
+
+template <typename T, typename TC, int LAYOUT>
+void launch_cam(const double* cams, int N, const void* I, int H, int W, int64_t ls, double x0, double y0,
+                double rcond, void* coef, hipStream_t s) {
+  const int64_t P = (int64_t)H * W;
+  hipLaunchKernelGGL((fit_perpixel_cam<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N,
+                     static_cast<const T*>(I), H, W, ls, x0, y0, rcond, static_cast<TC*>(coef));
+}
+
+template <typename T, typename TC>
+void launch_cam_l(int layout, const double* cams, int N, const void* I, int H, int W, int64_t ls, double x0,
+                  double y0, double rcond, void* coef, hipStream_t s) {
+  if (layout == RTI_COEF_PLANAR)
+    launch_cam<T, TC, RTI_COEF_PLANAR>(cams, N, I, H, W, ls, x0, y0, rcond, coef, s);
+  else
+    launch_cam<T, TC, RTI_COEF_PIXEL_MAJOR>(cams, N, I, H, W, ls, x0, y0, rcond, coef, s);
+}
+
+template <typename T>
+void launch_cam_c(int cdt, int layout, const double* cams, int N, const void* I, int H, int W, int64_t ls,
+                  double x0, double y0, double rcond, void* coef, hipStream_t s) {
+  if (cdt == RTI_F64)
+    launch_cam_l<T, double>(layout, cams, N, I, H, W, ls, x0, y0, rcond, coef, s);
+  else
+    launch_cam_l<T, float>(layout, cams, N, I, H, W, ls, x0, y0, rcond, coef, s);
+}
+
+template <typename T, typename TC, int LAYOUT>
+void launch_dirs(const float* lu, const float* lv, const void* I, int N, int64_t P, double rcond, void* coef,
+                 hipStream_t s) {
+  hipLaunchKernelGGL((fit_perpixel_dirs<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, lu, lv,
+                     static_cast<const T*>(I), N, P, rcond, static_cast<TC*>(coef));
+}
+
+template <typename T>
+void launch_dirs_c(int cdt, int layout, const float* lu, const float* lv, const void* I, int N, int64_t P,
+                   double rcond, void* coef, hipStream_t s) {
+  if (cdt == RTI_F64) {
+    if (layout == RTI_COEF_PLANAR)
+      launch_dirs<T, double, RTI_COEF_PLANAR>(lu, lv, I, N, P, rcond, coef, s);
+    else
+      launch_dirs<T, double, RTI_COEF_PIXEL_MAJOR>(lu, lv, I, N, P, rcond, coef, s);
+  } else {
+    if (layout == RTI_COEF_PLANAR)
+      launch_dirs<T, float, RTI_COEF_PLANAR>(lu, lv, I, N, P, rcond, coef, s);
+    else
+      launch_dirs<T, float, RTI_COEF_PIXEL_MAJOR>(lu, lv, I, N, P, rcond, coef, s);
+  }
+}
+
+int check_common(const char* fn, const void* I, int in_dtype, int N, int64_t P, void* coef, int coef_dtype,
+                 int coef_layout) {
+  if (!I || !coef) return fail(RTI_ERR_BAD_ARG, "%s: null pointer", fn);
+  if (N <= 0 || P <= 0) return fail(RTI_ERR_BAD_ARG, "%s: N and P must be positive", fn);
+  if (N < 6) return fail(RTI_ERR_BAD_ARG, "%s: %d lights < 6 PTM terms (analysis.py:298 raises ValueError)", fn, N);
+  if (in_dtype != RTI_F32 && in_dtype != RTI_U8 && in_dtype != RTI_I32)
+    return fail(RTI_ERR_UNSUPPORTED, "%s: input dtype %d", fn, in_dtype);
+  if (coef_dtype != RTI_F32 && coef_dtype != RTI_F64)
+    return fail(RTI_ERR_UNSUPPORTED, "%s: coef dtype %d", fn, coef_dtype);
+  if (coef_layout != RTI_COEF_PIXEL_MAJOR && coef_layout != RTI_COEF_PLANAR)
+    return fail(RTI_ERR_BAD_ARG, "%s: coef layout %d", fn, coef_layout);
+  return RTI_OK;
+}
+
+}  // namespace
+}  // namespace rti
+
+using namespace rti;
+
+extern "C" int rti_fit_perpixel_cam(const double* cams, int N, const void* I, int in_dtype, int H, int W,
+                                    int64_t light_stride, double x0, double y0, double rcond, void* coef,
+                                    int coef_dtype, int coef_layout, rti_stream_t stream) {
+  if (!cams) return fail(RTI_ERR_BAD_ARG, "rti_fit_perpixel_cam: null cams");
+  if (H <= 0 || W <= 0) return fail(RTI_ERR_BAD_ARG, "rti_fit_perpixel_cam: H and W must be positive");
+  const int64_t P = (int64_t)H * W;
+  int st = check_common("rti_fit_perpixel_cam", I, in_dtype, N, P, coef, coef_dtype, coef_layout);
+  if (st != RTI_OK) return st;
+  const int64_t ls = light_stride ? light_stride : P;
+  if (ls < P) return fail(RTI_ERR_BAD_ARG, "rti_fit_perpixel_cam: light_stride < H*W");
+  hipStream_t s = (hipStream_t)stream;
+  switch (in_dtype) {
+    case RTI_F32: launch_cam_c<float>(coef_dtype, coef_layout, cams, N, I, H, W, ls, x0, y0, rcond, coef, s); break;
+    case RTI_I32: launch_cam_c<int32_t>(coef_dtype, coef_layout, cams, N, I, H, W, ls, x0, y0, rcond, coef, s); break;
+    default: launch_cam_c<uint8_t>(coef_dtype, coef_layout, cams, N, I, H, W, ls, x0, y0, rcond, coef, s); break;
+  }
+  return check_launch("rti_fit_perpixel_cam");
+}
+
+extern "C" int rti_fit_perpixel_dirs(const float* lu, const float* lv, const void* I, int in_dtype, int N,
+                                     int64_t P, double rcond, void* coef, int coef_dtype, int coef_layout,
+                                     rti_stream_t stream) {
+  if (!lu || !lv) return fail(RTI_ERR_BAD_ARG, "rti_fit_perpixel_dirs: null lu/lv");
+  int st = check_common("rti_fit_perpixel_dirs", I, in_dtype, N, P, coef, coef_dtype, coef_layout);
+  if (st != RTI_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  switch (in_dtype) {
+    case RTI_F32: launch_dirs_c<float>(coef_dtype, coef_layout, lu, lv, I, N, P, rcond, coef, s); break;
+    case RTI_I32: launch_dirs_c<int32_t>(coef_dtype, coef_layout, lu, lv, I, N, P, rcond, coef, s); break;
+    default: launch_dirs_c<uint8_t>(coef_dtype, coef_layout, lu, lv, I, N, P, rcond, coef, s); break;
+  }
+  return check_launch("rti_fit_perpixel_dirs");
+}
+
+extern "C" int rti_light_dirs(const double* cams, int N, int H, int W, double x0, double y0, float* lu, float* lv,
+                              rti_stream_t stream) {
+  if (!cams || !lu || !lv) return fail(RTI_ERR_BAD_ARG, "rti_light_dirs: null pointer");
+  if (N <= 0 || H <= 0 || W <= 0) return fail(RTI_ERR_BAD_ARG, "rti_light_dirs: N, H, W must be positive");
+  const int64_t total = (int64_t)H * W * N;
+  hipLaunchKernelGGL(light_dirs, dim3(grid_1d(total, 256)), dim3(256), 0, (hipStream_t)stream, cams, N, W, total, x0,
+                     y0, lu, lv);
+  return check_launch("rti_light_dirs");
+}

@@ -1,0 +1,28 @@
+"""rti -- MI355X-native PTM/HSH reflectance fitter (drop-in for the hot path of
+bara96/Smartphone-based-RTI: analysis.py:196-411, interactive_relighting.py:11-39).
+
+    import rti
+    coef = rti.fit(I, lu, lv, basis="ptm")          # I: CUDA [N, H, W]
+    img = rti.relight(coef, 0.3, -0.2)               # [H, W]
+
+Compute runs in HIP kernels of librti.so (include/rti.h); importing this
+package does not touch the GPU.
+"""
+from . import _lib
+from ._lib import RTIError, RTILibraryMissing
+from .api import (BASES, basis_eval, basis_id, basis_terms, design_matrix, fit, fit_shared_into, light_dirs, pinv,
+                  relight)
+
+__all__ = ["BASES", "RTIError", "RTILibraryMissing", "basis_eval", "basis_id", "basis_terms", "design_matrix", "fit",
+           "fit_shared_into", "light_dirs", "pinv", "relight", "library_path", "load"]
+
+__version__ = "0.1.0"
+
+
+def library_path():
+    return _lib.LIB_PATH
+
+
+def load():
+    """Load librti.so now (raises RTILibraryMissing if it was not built)."""
+    return _lib.lib()

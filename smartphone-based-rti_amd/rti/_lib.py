@@ -1,0 +1,115 @@
+"""ctypes binding of ``librti.so`` (the C ABI declared in ``include/rti.h``).
+
+The library is built in-tree (``make -C smartphone-based-rti_amd`` or
+``__graft_entry__.build()``).  There is no fallback: if the library is missing
+every call raises ``RTILibraryMissing``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RTI_LIBRARY", os.path.join(HERE, "librti.so"))
+
+# ---- constants mirrored from include/rti.h (tests/test_abi.py checks they agree) ----
+RTI_OK = 0
+RTI_ERR_BAD_ARG = 1
+RTI_ERR_UNSUPPORTED = 2
+RTI_ERR_HIP = 3
+
+RTI_BASIS_PTM6 = 0
+RTI_BASIS_HSH16 = 1
+RTI_BASIS_HSH9 = 2
+
+RTI_F32 = 0
+RTI_U8 = 1
+RTI_I32 = 2
+RTI_F64 = 3
+
+RTI_COEF_PIXEL_MAJOR = 0
+RTI_COEF_PLANAR = 1
+
+RTI_OUT_EVAL_MAJOR = 0
+RTI_OUT_PIXEL_MAJOR = 1
+
+RTI_KERNEL_AUTO = 0
+RTI_KERNEL_VALU = 1
+RTI_KERNEL_MFMA = 2
+RTI_KERNEL_NONTEMPORAL = 0x100
+
+
+class RTILibraryMissing(ImportError):
+    pass
+
+
+class RTIError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__(message)
+        self.status = status
+
+
+_c_void_p = ctypes.c_void_p
+_c_int = ctypes.c_int
+_c_i64 = ctypes.c_int64
+_c_double = ctypes.c_double
+_c_float_p = ctypes.POINTER(ctypes.c_float)
+_c_double_p = ctypes.POINTER(ctypes.c_double)
+
+# name -> (restype, argtypes); every symbol of include/rti.h
+SIGNATURES = {
+    "rti_version": (_c_int, []),
+    "rti_status_string": (ctypes.c_char_p, [_c_int]),
+    "rti_last_error": (ctypes.c_char_p, []),
+    "rti_basis_terms": (_c_int, [_c_int]),
+    "rti_device_count": (_c_int, []),
+    "rti_design_matrix": (_c_int, [_c_int, _c_float_p, _c_float_p, _c_int, _c_double_p]),
+    "rti_pinv": (_c_int, [_c_int, _c_float_p, _c_float_p, _c_int, _c_double, _c_double_p]),
+    "rti_basis_eval": (_c_int, [_c_int, _c_double_p, _c_double_p, _c_int, _c_double_p]),
+    "rti_fit_shared": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_int, _c_i64, _c_int, _c_i64, _c_i64,
+                                _c_void_p, _c_int, _c_i64, _c_int, _c_void_p]),
+    "rti_fit_perpixel_cam": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_int, _c_int, _c_int, _c_i64, _c_double,
+                                      _c_double, _c_double, _c_void_p, _c_int, _c_int, _c_void_p]),
+    "rti_fit_perpixel_dirs": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_i64, _c_double,
+                                       _c_void_p, _c_int, _c_int, _c_void_p]),
+    "rti_light_dirs": (_c_int, [_c_void_p, _c_int, _c_int, _c_int, _c_double, _c_double, _c_void_p, _c_void_p,
+                                _c_void_p]),
+    "rti_relight": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_int, _c_void_p, _c_int, _c_void_p, _c_int,
+                             _c_int, _c_void_p]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib():
+    """Load librti.so once and declare every signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RTILibraryMissing(
+                    f"librti.so not found at {LIB_PATH}: build it with `make -C smartphone-based-rti_amd` "
+                    "(or __graft_entry__.build()); there is no CPU fallback")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(status, fn_name):
+    """Raise the Python exception matching an RTI status (RTI_OK passes)."""
+    if status == RTI_OK:
+        return
+    msg = lib().rti_last_error().decode(errors="replace") or fn_name
+    if status == RTI_ERR_BAD_ARG:
+        raise ValueError(msg)
+    if status == RTI_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RTIError(status, msg)

@@ -1,0 +1,281 @@
+"""Native API: ``fit()`` / ``relight()`` on CUDA (HIP) tensors through librti.so.
+
+Every compute call goes to a HIP kernel of ``librti.so`` on the caller's
+current torch stream.  Host-side work is limited to the k×N pseudo-inverse
+(``rti_pinv``, also native) and argument marshalling; there is no CPU path for
+the fit or the relight, and CPU tensors are rejected.
+
+Reference mapping (bara96/Smartphone-based-RTI @ v0):
+  * ``fit(mode="shared")``   — analysis.py:321-363 + :280-298, one pseudo-inverse
+    for every pixel (directional lights).
+  * ``fit(mode="perpixel")`` — the reference's own geometry: each pixel's light
+    list from compute_intensities (analysis.py:196-246), solved per pixel.
+  * ``relight()``            — analysis.py:300-315 (grid evaluation),
+    analysis.py:375-411 (int32 tables), interactive_relighting.py:25-36 (clip).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+BASES = {
+    "ptm": L.RTI_BASIS_PTM6, "ptm6": L.RTI_BASIS_PTM6,
+    "hsh": L.RTI_BASIS_HSH16, "hsh3": L.RTI_BASIS_HSH16, "hsh16": L.RTI_BASIS_HSH16,
+    "hsh2": L.RTI_BASIS_HSH9, "hsh9": L.RTI_BASIS_HSH9,
+}
+_KERNELS = {"auto": L.RTI_KERNEL_AUTO, "valu": L.RTI_KERNEL_VALU, "mfma": L.RTI_KERNEL_MFMA}
+_IN_DTYPES = {torch.float32: L.RTI_F32, torch.uint8: L.RTI_U8, torch.int32: L.RTI_I32}
+_COEF_DTYPES = {torch.float32: L.RTI_F32, torch.float64: L.RTI_F64}
+_OUT_DTYPES = {torch.float32: L.RTI_F32, torch.float64: L.RTI_F64, torch.int32: L.RTI_I32, torch.uint8: L.RTI_U8}
+
+
+def basis_id(basis):
+    if isinstance(basis, int):
+        return basis
+    try:
+        return BASES[basis.lower()]
+    except (KeyError, AttributeError):
+        raise ValueError(f"unknown basis {basis!r}; expected one of {sorted(BASES)}") from None
+
+
+def basis_terms(basis):
+    return L.lib().rti_basis_terms(basis_id(basis))
+
+
+def _f32_host(x, name):
+    a = np.ascontiguousarray(np.asarray(x.detach().cpu() if torch.is_tensor(x) else x, dtype=np.float32).ravel())
+    if a.size == 0:
+        raise ValueError(f"{name} is empty")
+    return a
+
+
+def _fptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _dptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def design_matrix(lu, lv, basis="ptm"):
+    """Host fp64 design matrix [N, k] (analysis.py:280-291 for PTM)."""
+    lu, lv = _f32_host(lu, "lu"), _f32_host(lv, "lv")
+    if lu.size != lv.size:
+        raise ValueError("lu and lv differ in length")
+    b = basis_id(basis)
+    A = np.empty((lu.size, basis_terms(b)), dtype=np.float64)
+    L.check(L.lib().rti_design_matrix(b, _fptr(lu), _fptr(lv), lu.size, _dptr(A)), "rti_design_matrix")
+    return A
+
+
+def pinv(lu, lv, basis="ptm", rcond=None):
+    """Host fp64 pseudo-inverse [k, N] of the shared design (analysis.py:293-298).
+
+    ``rcond=None`` keeps the reference's semantics (no threshold)."""
+    lu, lv = _f32_host(lu, "lu"), _f32_host(lv, "lv")
+    if lu.size != lv.size:
+        raise ValueError("lu and lv differ in length")
+    b = basis_id(basis)
+    out = np.empty((basis_terms(b), lu.size), dtype=np.float64)
+    rc = -1.0 if rcond is None else float(rcond)
+    L.check(L.lib().rti_pinv(b, _fptr(lu), _fptr(lv), lu.size, rc, _dptr(out)), "rti_pinv")
+    return out
+
+
+def basis_eval(lu, lv, basis="ptm"):
+    """Host fp64 basis values [E, k] at (lu, lv)."""
+    lu = np.ascontiguousarray(np.asarray(lu, np.float64).ravel())
+    lv = np.ascontiguousarray(np.asarray(lv, np.float64).ravel())
+    b = basis_id(basis)
+    out = np.empty((lu.size, basis_terms(b)), np.float64)
+    L.check(L.lib().rti_basis_eval(b, _dptr(lu), _dptr(lv), lu.size, _dptr(out)), "rti_basis_eval")
+    return out
+
+
+def _require_cuda(t, name):
+    if not torch.is_tensor(t) or not t.is_cuda:
+        raise ValueError(f"{name} must be a CUDA (HIP) tensor: librti runs only on the GPU, there is no CPU path")
+
+
+def _stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _layout_id(layout):
+    if layout in ("pixel", "pixel_major", L.RTI_COEF_PIXEL_MAJOR):
+        return L.RTI_COEF_PIXEL_MAJOR
+    if layout in ("planar", L.RTI_COEF_PLANAR):
+        return L.RTI_COEF_PLANAR
+    raise ValueError(f"unknown coefficient layout {layout!r} (expected 'pixel' or 'planar')")
+
+
+def fit_shared_into(pinv_dev, I, coef, *, k, layout="pixel", kernel="auto", nontemporal=False):
+    """Launch ``rti_fit_shared`` on preallocated tensors (no allocation, graph-capturable).
+
+    pinv_dev: CUDA fp32 [k, N]; I: CUDA [C, N, P] or [N, P] (contiguous
+    light-major, fp32/u8/int32); coef: CUDA fp32 [C, P, k] / [C, k, P]."""
+    if I.dim() == 2:
+        C, (N, P) = 1, I.shape
+    else:
+        C, N, P = I.shape
+    kern = _KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+    if nontemporal:
+        kern |= L.RTI_KERNEL_NONTEMPORAL
+    st = L.lib().rti_fit_shared(_vp(pinv_dev), k, N, _vp(I), _IN_DTYPES[I.dtype], P, C, P, N * P, _vp(coef),
+                                _layout_id(layout), P * k, kern, _stream_of(I))
+    L.check(st, "rti_fit_shared")
+    return coef
+
+
+def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=None, origin=(0.0, 0.0),
+        layout="pixel", kernel="auto", coef_dtype=torch.float32, nontemporal=False):
+    """Fit per-pixel reflectance coefficients on the GPU.
+
+    mode="shared" (the north_star path; directional lights, one (lu, lv) per light):
+        I: CUDA tensor [N, H, W], [N, P] or [C, N, H, W] (light-major), fp32/u8/int32.
+        lu, lv: N light directions (host or device).  Returns fp32 coefficients
+        [.., H, W, k] (layout="pixel") or [.., k, H, W] (layout="planar").
+    mode="perpixel" (the reference's geometry, PTM only):
+        either cams=[N, 3] camera positions with I light-major [N, H, W]
+        (directions generated in-kernel, pixel (x, y) at origin + (x, y, 0)),
+        or lu, lv, I pixel-major [H, W, N] exactly as compute_intensities returns
+        them (analysis.py:217-219).  Coefficients in coef_dtype (fp32 or fp64).
+    """
+    _require_cuda(I, "I")
+    cl = _layout_id(layout)
+    if mode == "shared":
+        if lu is None or lv is None:
+            raise ValueError("shared mode needs lu and lv (one direction per light)")
+        b = basis_id(basis)
+        k = basis_terms(b)
+        lead = I.shape[:-2] if I.dim() >= 3 else I.shape[:-1]
+        if I.dim() == 2:
+            N, P = I.shape
+            C, spatial = 1, (P,)
+        elif I.dim() == 3:
+            N, H, W = I.shape
+            C, P, spatial = 1, H * W, (H, W)
+        elif I.dim() == 4:
+            C, N, H, W = I.shape
+            P, spatial = H * W, (H, W)
+        else:
+            raise ValueError("I must be [N, P], [N, H, W] or [C, N, H, W]")
+        del lead
+        if N < k:
+            raise ValueError(f"shapes not aligned: {N} lights < {k} basis terms (analysis.py:298)")
+        pv = pinv(lu, lv, b, rcond)
+        if pv.shape[1] != N:
+            raise ValueError(f"{pv.shape[1]} light directions for {N} intensity planes")
+        pinv_dev = torch.as_tensor(pv.astype(np.float32), device=I.device)
+        Ic = I.contiguous().reshape(C, N, P)
+        shape = (C, P, k) if cl == L.RTI_COEF_PIXEL_MAJOR else (C, k, P)
+        coef = torch.empty(shape, dtype=torch.float32, device=I.device)
+        fit_shared_into(pinv_dev, Ic, coef, k=k, layout=cl, kernel=kernel, nontemporal=nontemporal)
+        if cl == L.RTI_COEF_PIXEL_MAJOR:
+            out = coef.reshape((C,) + spatial + (k,))
+        else:
+            out = coef.reshape((C, k) + spatial)
+        return out if I.dim() == 4 else out[0]
+    if mode != "perpixel":
+        raise ValueError(f"unknown mode {mode!r} (expected 'shared' or 'perpixel')")
+    if basis_id(basis) != L.RTI_BASIS_PTM6:
+        raise NotImplementedError("per-pixel mode is the reference's PTM-6 path")
+    cdt = _COEF_DTYPES.get(coef_dtype)
+    if cdt is None:
+        raise ValueError("coef_dtype must be torch.float32 or torch.float64")
+    rc = -1.0 if rcond is None else float(rcond)
+    if cams is not None:
+        if I.dim() != 3:
+            raise ValueError("per-pixel camera mode needs I light-major [N, H, W]")
+        N, H, W = I.shape
+        cams_d = torch.as_tensor(np.asarray(cams.detach().cpu() if torch.is_tensor(cams) else cams, np.float64),
+                                 device=I.device).contiguous()
+        if cams_d.shape != (N, 3):
+            raise ValueError(f"cams must be [{N}, 3]")
+        Ic = I.contiguous()
+        shape = (H, W, 6) if cl == L.RTI_COEF_PIXEL_MAJOR else (6, H, W)
+        coef = torch.empty(shape, dtype=coef_dtype, device=I.device)
+        st = L.lib().rti_fit_perpixel_cam(_vp(cams_d), N, _vp(Ic), _IN_DTYPES[Ic.dtype], H, W, H * W,
+                                          float(origin[0]), float(origin[1]), rc, _vp(coef), cdt, cl, _stream_of(I))
+        L.check(st, "rti_fit_perpixel_cam")
+        return coef
+    if lu is None or lv is None:
+        raise ValueError("per-pixel mode needs cams=[N,3] or per-pixel lu, lv [H, W, N]")
+    lu_d = torch.as_tensor(lu, device=I.device).to(torch.float32).contiguous()
+    lv_d = torch.as_tensor(lv, device=I.device).to(torch.float32).contiguous()
+    if lu_d.shape != I.shape or lv_d.shape != I.shape:
+        raise ValueError("per-pixel lu, lv and I must share the pixel-major shape [.., N]")
+    N = I.shape[-1]
+    spatial = tuple(I.shape[:-1])
+    P = int(np.prod(spatial)) if spatial else 1
+    Ic = I.contiguous()
+    shape = spatial + (6,) if cl == L.RTI_COEF_PIXEL_MAJOR else (6,) + spatial
+    coef = torch.empty(shape, dtype=coef_dtype, device=I.device)
+    st = L.lib().rti_fit_perpixel_dirs(_vp(lu_d), _vp(lv_d), _vp(Ic), _IN_DTYPES[Ic.dtype], N, P, rc, _vp(coef), cdt,
+                                       cl, _stream_of(I))
+    L.check(st, "rti_fit_perpixel_dirs")
+    return coef
+
+
+def light_dirs(cams, H, W, origin=(0.0, 0.0), device="cuda"):
+    """compute_intensities' light vectors on the GPU: (lu, lv) fp32 [H, W, N]."""
+    cams_d = torch.as_tensor(np.asarray(cams.detach().cpu() if torch.is_tensor(cams) else cams, np.float64),
+                             device=device).contiguous()
+    _require_cuda(cams_d, "cams")
+    N = cams_d.shape[0]
+    lu = torch.empty((H, W, N), dtype=torch.float32, device=cams_d.device)
+    lv = torch.empty_like(lu)
+    st = L.lib().rti_light_dirs(_vp(cams_d), N, H, W, float(origin[0]), float(origin[1]), _vp(lu), _vp(lv),
+                                _stream_of(cams_d))
+    L.check(st, "rti_light_dirs")
+    return lu, lv
+
+
+def relight(coef, lu, lv, basis="ptm", *, layout="pixel", out_dtype=torch.float32, out_layout="eval"):
+    """Evaluate coefficient maps at light directions on the GPU.
+
+    coef: CUDA fp32/fp64, [H, W, k] / [P, k] (layout="pixel") or [k, H, W] /
+    [k, P] (layout="planar").  lu, lv: scalars or E directions.
+    Returns [E, H, W] (out_layout="eval") or [H, W, E] (out_layout="pixel"),
+    squeezed to [H, W] for a single scalar direction.  out_dtype int32 gives
+    the reference's truncated tables, uint8 its clipped display values."""
+    _require_cuda(coef, "coef")
+    b = basis_id(basis)
+    k = basis_terms(b)
+    cl = _layout_id(layout)
+    cdt = _COEF_DTYPES.get(coef.dtype)
+    if cdt is None:
+        raise ValueError("coef must be float32 or float64")
+    odt = _OUT_DTYPES.get(out_dtype)
+    if odt is None:
+        raise ValueError("out_dtype must be float32, float64, int32 or uint8")
+    if cl == L.RTI_COEF_PIXEL_MAJOR:
+        if coef.shape[-1] != k:
+            raise ValueError(f"coef last dim {coef.shape[-1]} != {k} terms")
+        spatial = tuple(coef.shape[:-1])
+    else:
+        if coef.shape[0] != k:
+            raise ValueError(f"coef first dim {coef.shape[0]} != {k} terms")
+        spatial = tuple(coef.shape[1:])
+    P = int(np.prod(spatial))
+    scalar = np.ndim(lu) == 0 and np.ndim(lv) == 0
+    luv = np.stack([np.asarray(lu, np.float64).ravel(), np.asarray(lv, np.float64).ravel()], -1)
+    E = luv.shape[0]
+    luv_d = torch.as_tensor(np.ascontiguousarray(luv), device=coef.device)
+    ol = L.RTI_OUT_EVAL_MAJOR if out_layout == "eval" else L.RTI_OUT_PIXEL_MAJOR
+    shape = (E,) + spatial if ol == L.RTI_OUT_EVAL_MAJOR else spatial + (E,)
+    out = torch.empty(shape, dtype=out_dtype, device=coef.device)
+    c = coef.contiguous()
+    st = L.lib().rti_relight(_vp(c), cdt, b, P, cl, _vp(luv_d), E, _vp(out), odt, ol, _stream_of(c))
+    L.check(st, "rti_relight")
+    if scalar:
+        return out[0] if ol == L.RTI_OUT_EVAL_MAJOR else out[..., 0]
+    return out

@@ -1,0 +1,171 @@
+"""Reference-signature adapters (bara96/Smartphone-based-RTI @ v0, analysis.py).
+
+Same names, argument meaning, return layout and error behaviour as the
+reference's hot-path functions, with the compute done by librti's HIP kernels:
+
+==============================  ===========================================  ==============================
+reference                       file:line                                    HIP path used here
+==============================  ===========================================  ==============================
+compute_intensities             analysis.py:196-246                          rti_light_dirs
+_interpolate_PTM                analysis.py:263-317                          rti_fit_perpixel_dirs (P=1) + rti_relight
+interpolate_intensities (PTM)   analysis.py:321-372                          rti_fit_perpixel_dirs + rti_relight (pixel-major)
+prepare_images_data             analysis.py:375-411                          layout adapter (torch); native: relight_tables
+relighting_event lookup         interactive_relighting.py:11-39              table lookup + clip (host, one image)
+==============================  ===========================================  ==============================
+
+Inputs may be NumPy arrays (as in the reference) or tensors; outputs are NumPy
+arrays with the reference's dtypes.  The reference returns nested lists; here
+the same indexing ([y][x][ly][lx], [ly][lx][y][x]) works on ndarrays.
+Differences, by design:
+  * the ROI size is the data's size, not ``constants.ROI_DIAMETER``;
+  * the RBF branch (``interpolate_PTM=False``, the reference's default) is the
+    next row of SURVEY §8(f) and raises ``NotImplementedError`` for now;
+  * the debug plots of ``first_only=True`` are not drawn (first pixel only is kept).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import api
+
+INTERPOLATION_PARAM = 0.02  # constants.py:11
+
+
+def _device(device=None):
+    if device is not None:
+        return torch.device(device)
+    if not torch.cuda.is_available():
+        raise RuntimeError("rti.compat needs a HIP device (librti has no CPU path)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def grid_axis(step=INTERPOLATION_PARAM):
+    """``np.around(np.mgrid[-1:1:step, -1:1:step], 2)`` axis (analysis.py:345-347, :390-393)."""
+    _, xi = np.mgrid[-1:1:step, -1:1:step]
+    return np.around(xi, decimals=2)[0]
+
+
+def _grid_luv(xy_fine):
+    xf = np.asarray(xy_fine, np.float64).ravel()
+    lu = np.tile(xf, xf.size)          # e = v*G + u  ->  (lu = xf[u], lv = xf[v])
+    lv = np.repeat(xf, xf.size)
+    return xf.size, lu, lv
+
+
+def compute_intensities(data, first_only=False, origin=(0.0, 0.0), device=None):
+    """analysis.py:196-246: list of (V uint8[R,R], camera f64[3]) -> (lx f32, ly f32, I int32), each [R,R,N]."""
+    if data is None or len(data) <= 0:
+        raise Exception("Error computing intensities: results are empty")
+    dev = _device(device)
+    frames = [np.asarray(f) for f, _ in data]
+    cams = np.stack([np.asarray(c, np.float64).ravel()[:3] for _, c in data])
+    R = frames[0].shape[0]
+    if first_only:
+        R = 1
+    lu, lv = api.light_dirs(cams, R, R, origin=origin, device=dev)
+    inten = np.stack([f[:R, :R] for f in frames], axis=-1).astype(np.int32)
+    torch.cuda.synchronize(dev)
+    return lu.cpu().numpy(), lv.cpu().numpy(), inten
+
+
+def _perpixel_coefs(lx, ly, inten, dev):
+    lx_t = torch.as_tensor(np.ascontiguousarray(lx, np.float32), device=dev)
+    ly_t = torch.as_tensor(np.ascontiguousarray(ly, np.float32), device=dev)
+    it = np.asarray(inten)
+    if it.dtype not in (np.float32, np.int32, np.uint8):
+        it = it.astype(np.int32)
+    I_t = torch.as_tensor(np.ascontiguousarray(it), device=dev)
+    return api.fit(I_t, lx_t, ly_t, basis="ptm", mode="perpixel", coef_dtype=torch.float64)
+
+
+def _interpolate_PTM(x_coarse, y_coarse, xy_fine, intensity_values, device=None):
+    """analysis.py:263-317: one pixel's PTM fit evaluated on xy_fine × xy_fine -> f64 [G, G] ([lv][lu])."""
+    dev = _device(device)
+    n = len(intensity_values)
+    if n < 6:
+        raise ValueError(f"shapes not aligned: {n} lights < 6 PTM terms")
+    coef = _perpixel_coefs(np.asarray(x_coarse).reshape(1, n), np.asarray(y_coarse).reshape(1, n),
+                           np.asarray(intensity_values).reshape(1, n), dev)
+    G, lu, lv = _grid_luv(xy_fine)
+    out = api.relight(coef, lu, lv, basis="ptm", out_dtype=torch.float64, out_layout="pixel")
+    return out.reshape(G, G).cpu().numpy()
+
+
+def interpolate_intensities(data, interpolate_PTM=False, first_only=False, device=None):
+    """analysis.py:321-372 -> ndarray [R, R, G, G] f64 indexed [y][x][ly][lx]."""
+    if data is None or len(data) != 3:
+        raise Exception("Error computing interpolation: results are empty or invalid")
+    if not interpolate_PTM:
+        raise NotImplementedError("linear RBF interpolation (analysis.py:249-260) is the next row (SURVEY §8(f)-1)")
+    lx, ly, inten = (np.asarray(d) for d in data)
+    R = 1 if first_only else lx.shape[0]
+    lx, ly, inten = lx[:R, :R], ly[:R, :R], inten[:R, :R]
+    if lx.shape[-1] < 6:
+        raise ValueError(f"shapes not aligned: {lx.shape[-1]} lights < 6 PTM terms")
+    dev = _device(device)
+    coef = _perpixel_coefs(lx, ly, inten, dev)
+    G, lu, lv = _grid_luv(grid_axis())
+    out = api.relight(coef, lu, lv, basis="ptm", out_dtype=torch.float64, out_layout="pixel")
+    return out.reshape(R, R, G, G).cpu().numpy()
+
+
+def prepare_images_data(data, first_only=False, device=None):
+    """analysis.py:375-411: [y][x][ly][lx] f64 -> [ly][lx][y][x] int32 (C truncation; NaN -> INT32_MIN)."""
+    if data is None or len(data) <= 0:
+        raise Exception("Error preparing images: results are empty")
+    dev = _device(device)
+    d = torch.as_tensor(np.asarray(data, np.float64), device=dev)
+    if first_only:
+        d = d[:1, :1]
+    t = d.permute(2, 3, 0, 1).contiguous()
+    ok = (t >= -2147483648.0) & (t < 2147483648.0)
+    out = torch.where(ok, torch.trunc(torch.where(ok, t, torch.zeros_like(t))),
+                      torch.full_like(t, -2147483648.0)).to(torch.int32)
+    return out.cpu().numpy()
+
+
+def relight_tables(coef, step=INTERPOLATION_PARAM, layout="pixel"):
+    """Native fused replacement of interpolate_intensities + prepare_images_data:
+    coefficient maps [H, W, 6] (fp64 for bit-faithful grids) -> int32 [G, G, H, W]."""
+    G, lu, lv = _grid_luv(grid_axis(step))
+    out = api.relight(coef, lu, lv, basis="ptm", layout=layout, out_dtype=torch.int32, out_layout="eval")
+    spatial = out.shape[1:]
+    return out.reshape((G, G) + tuple(spatial))
+
+
+def draw_light_roi_position(given_x, given_y, shape, to_light_vector=False):
+    """Cursor <-> light-vector mapping (Utils/utilities.py:357-381)."""
+    h, w = shape
+    if to_light_vector:
+        lx = round(2 * (given_x / w) - 1, 2)
+        ly = round(2 * (given_y / h) - 1, 2)
+        if lx >= 0.99:
+            lx = 0.98
+        if ly >= 0.99:
+            ly = 0.98
+        return lx, ly
+    return int(2 * (1 + given_x) * 100), int(2 * (1 + given_y) * 100)
+
+
+def table_index(l):
+    """interactive_relighting.py:25-26."""
+    return round((1 + l) / 2 * 100)
+
+
+def relight_lookup(tables, x, y, shape):
+    """relighting_event's table lookup + clip (interactive_relighting.py:22-36) -> int32 image [R, R].
+
+    The reference clips the looked-up table IN PLACE (:35-36); this returns a
+    clipped copy and leaves ``tables`` unchanged."""
+    lx, ly = draw_light_roi_position(x, y, shape, to_light_vector=True)
+    vals = np.array(tables[table_index(ly)][table_index(lx)], copy=True)
+    vals[vals > 255] = 255
+    vals[vals <= 0] = 0
+    return vals
+
+
+def relight_at_cursor(coef, x, y, shape, basis="ptm"):
+    """Continuous relighting: cursor -> (lx, ly) -> uint8 V image from coefficients."""
+    lx, ly = draw_light_roi_position(x, y, shape, to_light_vector=True)
+    return api.relight(coef, lx, ly, basis=basis, out_dtype=torch.uint8)

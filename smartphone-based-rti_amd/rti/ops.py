@@ -1,0 +1,53 @@
+"""PyTorch custom ops over the C ABI: ``torch.ops.rti.fit_shared`` / ``torch.ops.rti.relight``.
+
+They let the fit and relight kernels sit inside torch programs (and
+``torch.library`` fake-tensor tracing) while the compute stays in librti's
+HIP kernels on the current stream.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from . import api
+
+
+@torch.library.custom_op("rti::fit_shared", mutates_args=())
+def fit_shared(pinv: torch.Tensor, I: torch.Tensor, planar: bool = False, kernel: int = 0) -> torch.Tensor:
+    """coef = pinv (fp32 [k, N]) applied to I (CUDA [N, P] or [C, N, P]) -> [C?, P, k] or [C?, k, P]."""
+    api._require_cuda(I, "I")
+    api._require_cuda(pinv, "pinv")
+    if pinv.dtype != torch.float32:
+        raise ValueError("pinv must be float32")
+    k = pinv.shape[0]
+    I3 = I.contiguous() if I.dim() == 3 else I.contiguous().unsqueeze(0)
+    C, N, P = I3.shape
+    if pinv.shape[1] != N:
+        raise ValueError(f"pinv is [{k}, {pinv.shape[1]}] but I has {N} lights")
+    shape = (C, k, P) if planar else (C, P, k)
+    coef = torch.empty(shape, dtype=torch.float32, device=I.device)
+    api.fit_shared_into(pinv.contiguous(), I3, coef, k=k, layout="planar" if planar else "pixel", kernel=kernel)
+    return coef if I.dim() == 3 else coef[0]
+
+
+@fit_shared.register_fake
+def _(pinv, I, planar=False, kernel=0):
+    k = pinv.shape[0]
+    P = I.shape[-1]
+    shape = (k, P) if planar else (P, k)
+    if I.dim() == 3:
+        shape = (I.shape[0],) + shape
+    return I.new_empty(shape, dtype=torch.float32)
+
+
+@torch.library.custom_op("rti::relight", mutates_args=())
+def relight(coef: torch.Tensor, luv: torch.Tensor, basis: int = L.RTI_BASIS_PTM6) -> torch.Tensor:
+    """coef CUDA [P, k] (fp32/fp64), luv [E, 2] -> [E, P] in coef's dtype."""
+    lu = luv[:, 0].detach().cpu().double().numpy()
+    lv = luv[:, 1].detach().cpu().double().numpy()
+    return api.relight(coef, lu, lv, basis=basis, out_dtype=coef.dtype)
+
+
+@relight.register_fake
+def _(coef, luv, basis=L.RTI_BASIS_PTM6):
+    return coef.new_empty((luv.shape[0], coef.shape[0]))

@@ -1,0 +1,123 @@
+"""C ABI checks that need no GPU: librti.so loads, exports every symbol of
+include/rti.h, its constants match the Python mirror, and the host half
+(design matrix, pseudo-inverse, basis) agrees with the oracle."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import rti
+import rti_oracle as o
+from conftest import ROOT, golden
+from rti import _lib as L
+
+HEADER = os.path.join(ROOT, "include", "rti.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rti_[a-z0-9_]+)\s*\(", src)))
+
+
+def header_defines():
+    return dict((m.group(1), int(m.group(2), 0))
+                for m in re.finditer(r"#define\s+(RTI_[A-Z0-9_]+)\s+(0x[0-9a-fA-F]+|\d+)", open(HEADER).read()))
+
+
+def test_library_exports_every_header_symbol():
+    lib = rti.load()
+    names = header_functions()
+    assert len(names) >= 12
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(L.SIGNATURES), "Python signature table out of sync with include/rti.h"
+
+
+def test_constants_match_header():
+    for name, value in header_defines().items():
+        assert getattr(L, name) == value, name
+
+
+def test_info_functions():
+    lib = rti.load()
+    assert lib.rti_version() == 100
+    assert lib.rti_status_string(0) == b"ok"
+    assert lib.rti_basis_terms(L.RTI_BASIS_PTM6) == 6
+    assert lib.rti_basis_terms(L.RTI_BASIS_HSH16) == 16
+    assert lib.rti_basis_terms(L.RTI_BASIS_HSH9) == 9
+    assert lib.rti_basis_terms(99) == -1
+
+
+def test_pinv_matches_oracle_and_reference_goldens():
+    d = golden("ptm_shared_256x256_N20.npz")
+    pv = rti.pinv(d["lu"], d["lv"])
+    ref = o.pinv_shared("ptm", d["lu"], d["lv"])
+    assert np.abs(pv - ref).max() <= 1e-13 * np.abs(ref).max()
+    # applied to the golden intensities, the host pinv reproduces the reference's coefficients
+    I = d["I"].astype(np.float64).reshape(20, -1)
+    coef = (pv @ I).T.reshape(d["coef"].shape)
+    scale = np.abs(d["coef"]).max(-1, keepdims=True)
+    assert (np.abs(coef - d["coef"]) / scale).max() < 1e-12
+
+
+@pytest.mark.parametrize("basis,k", [("hsh", 16), ("hsh9", 9)])
+def test_hsh_design_and_pinv_match_oracle(basis, k):
+    lu, lv = o.synth_dirs(120, 7)
+    A = rti.design_matrix(lu, lv, basis)
+    A0 = o.design("hsh", lu, lv)[:, :k]
+    assert A.shape == (120, k)
+    assert np.abs(A - A0).max() < 1e-13
+    pv = rti.pinv(lu, lv, basis)
+    assert np.abs(pv - np.linalg.pinv(A0)).max() < 1e-11 * np.abs(pv).max()
+
+
+def test_ptm_design_uses_float32_monomials():
+    lu, lv = o.synth_dirs(50, 3)
+    A = rti.design_matrix(lu, lv)
+    A0 = o.ptm_design(lu, lv)
+    # the reference forms lu**2 with glibc powf (1-ulp differences from x*x are allowed)
+    assert np.abs(A - A0).max() <= 2 * np.finfo(np.float32).eps
+    assert np.array_equal(A[:, 2:], A0[:, 2:])
+
+
+def test_pinv_rank_deficient_and_rcond():
+    e = golden("ptm_edge.npz")
+    pv = rti.pinv(e["singular_lu"], e["singular_lv"])
+    assert not np.isfinite(pv).all()  # reference semantics: division by a zero singular value
+    pv = rti.pinv(e["singular_lu"], e["singular_lv"], rcond=1e-10)
+    assert np.isfinite(pv).all()
+    A = o.ptm_design(e["singular_lu"], e["singular_lv"])
+    assert np.abs(pv - np.linalg.pinv(A, rcond=1e-10)).max() < 1e-10 * np.abs(pv).max()
+
+
+def test_bad_arguments_raise_like_reference():
+    lu, lv = o.synth_dirs(5, 1)
+    with pytest.raises(ValueError):
+        rti.pinv(lu, lv)  # N < 6: the reference raises ValueError (analysis.py:298)
+    with pytest.raises(ValueError):
+        rti.pinv(lu, lv[:4])
+    with pytest.raises(ValueError):
+        rti.basis_id("rbf")
+
+
+def test_fit_rejects_cpu_tensors():
+    import torch
+
+    I = torch.zeros((8, 4, 4))
+    lu, lv = o.synth_dirs(8, 1)
+    with pytest.raises(ValueError, match="CUDA"):
+        rti.fit(I, lu, lv)
+    with pytest.raises(ValueError, match="CUDA"):
+        rti.relight(torch.zeros((4, 4, 6)), 0.1, 0.2)
+
+
+def test_basis_eval_matches_oracle():
+    lu, lv = o.synth_dirs(64, 9, radius=1.0)
+    lu = lu.astype(np.float64)
+    lv = lv.astype(np.float64)
+    B = rti.basis_eval(lu, lv, "hsh")
+    assert np.abs(B - o.hsh_basis(lu, lv)).max() < 1e-13
+    P = rti.basis_eval(lu, lv, "ptm")
+    assert np.array_equal(P, np.stack([lu * lu, lv * lv, lu * lv, lu, lv, np.ones_like(lu)], -1))

@@ -1,0 +1,138 @@
+"""GPU parity of the shared-direction fit (rti_fit_shared) against the oracle
+and the reference's golden coefficients.  Tolerance:
+|c - c_ref| <= 1e-4 * max_k |c_ref,k| per pixel, fp32 arithmetic."""
+import numpy as np
+import pytest
+import torch
+
+import rti
+import rti_oracle as o
+from conftest import coef_close, golden
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = ["valu", "mfma"]
+
+
+def to_dev(a, dev, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(dev, dtype)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_golden_256x256_N20(cuda, kernel):
+    d = golden("ptm_shared_256x256_N20.npz")
+    I = to_dev(d["I"], cuda)  # [20, 256, 256] light-major
+    coef = rti.fit(I, d["lu"], d["lv"], kernel=kernel).cpu().numpy()
+    err, ok = coef_close(coef, d["coef"])
+    assert ok, err
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("in_dtype", [torch.float32, torch.uint8, torch.int32])
+@pytest.mark.parametrize("layout", ["pixel", "planar"])
+def test_dtypes_layouts(cuda, kernel, in_dtype, layout):
+    d = golden("ptm_shared_256x256_N20.npz")
+    I = torch.as_tensor(d["I"]).to(cuda).to(in_dtype)
+    coef = rti.fit(I, d["lu"], d["lv"], kernel=kernel, layout=layout).cpu().numpy()
+    if layout == "planar":
+        coef = np.moveaxis(coef, 0, -1)
+    err, ok = coef_close(coef, d["coef"])
+    assert ok, err
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("hw,n", [((1, 1), 6), ((3, 5), 7), ((17, 33), 13), ((64, 65), 37), ((31, 128), 50),
+                                  ((8, 8), 200)])
+def test_ragged_shapes_vs_oracle(cuda, kernel, hw, n):
+    h, w = hw
+    lu, lv = o.synth_dirs(n, n)
+    I = o.synth_intensities(h, w, lu, lv, seed=h * 1000 + w)
+    ref = o.fit_shared(I, o.pinv_shared("ptm", lu, lv)).reshape(h, w, 6)
+    coef = rti.fit(to_dev(I, cuda), lu, lv, kernel=kernel).cpu().numpy()
+    err, ok = coef_close(coef, ref)
+    assert ok, err
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("basis,k", [("hsh", 16), ("hsh9", 9)])
+def test_hsh_vs_oracle(cuda, kernel, basis, k):
+    lu, lv = o.synth_dirs(60, 11)
+    I = o.synth_intensities(48, 40, lu, lv, seed=3, basis="hsh")
+    A = o.design("hsh", lu, lv)[:, :k]
+    ref = (np.linalg.pinv(A) @ I.reshape(60, -1).astype(np.float64)).T.reshape(48, 40, k)
+    coef = rti.fit(to_dev(I, cuda), lu, lv, basis=basis, kernel=kernel).cpu().numpy()
+    err, ok = coef_close(coef, ref)
+    assert ok, err
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_rgb_channels(cuda, kernel):
+    lu, lv = o.synth_dirs(40, 4)
+    planes = [o.synth_intensities(32, 48, lu, lv, seed=s) for s in (1, 2, 3)]
+    I = np.stack(planes)  # [3, N, H, W]
+    pv = o.pinv_shared("ptm", lu, lv)
+    coef = rti.fit(to_dev(I, cuda), lu, lv, kernel=kernel).cpu().numpy()
+    assert coef.shape == (3, 32, 48, 6)
+    for c in range(3):
+        err, ok = coef_close(coef[c], o.fit_shared(planes[c], pv).reshape(32, 48, 6))
+        assert ok, (c, err)
+
+
+def test_rank_deficient_gives_nonfinite(cuda):
+    e = golden("ptm_edge.npz")
+    I = to_dev(np.tile(e["singular_I"].astype(np.float32)[:, None], (1, 64)), cuda)
+    coef = rti.fit(I, e["singular_lu"], e["singular_lv"]).cpu().numpy()
+    assert not np.isfinite(coef).all()
+    coef = rti.fit(I, e["singular_lu"], e["singular_lv"], rcond=1e-10).cpu().numpy()
+    assert np.isfinite(coef).all()
+
+
+def test_edge_goldens_single_pixels(cuda):
+    e = golden("ptm_edge.npz")
+    for name in ("exact6", "n200"):
+        I = to_dev(e[f"{name}_I"].astype(np.float32)[:, None], cuda)
+        coef = rti.fit(I, e[f"{name}_lu"], e[f"{name}_lv"]).cpu().numpy()
+        err, ok = coef_close(coef, e[f"{name}_coef"][None])
+        assert ok, (name, err)
+
+
+def test_too_few_lights_raises(cuda):
+    lu, lv = o.synth_dirs(5, 1)
+    with pytest.raises(ValueError):
+        rti.fit(torch.zeros((5, 4, 4), device=cuda), lu, lv)
+
+
+def test_custom_op_matches_api(cuda):
+    from rti import ops  # noqa: F401  registers torch.ops.rti.*
+
+    d = golden("ptm_shared_256x256_N20.npz")
+    I = to_dev(d["I"], cuda).reshape(20, -1)
+    pv = torch.as_tensor(rti.pinv(d["lu"], d["lv"]).astype(np.float32), device=cuda)
+    coef = torch.ops.rti.fit_shared(pv, I).cpu().numpy().reshape(d["coef"].shape)
+    err, ok = coef_close(coef, d["coef"])
+    assert ok, err
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_full_size_4k_n100_properties(cuda, kernel):
+    """BASELINE configs[2] size (3840x2160, N=100): exact recovery + sampled fp64 parity + linearity."""
+    H, W, N = 2160, 3840, 100
+    lu, lv = o.synth_dirs(N, 2)
+    g = torch.Generator(device=cuda).manual_seed(0)
+    a_true = torch.rand((6, H * W), generator=g, device=cuda, dtype=torch.float32) * 100 - 50
+    B = torch.as_tensor(o.ptm_design(lu, lv), device=cuda, dtype=torch.float32)  # [N, 6]
+    I = (B @ a_true).reshape(N, H, W)  # noise-free: the fit must return a_true
+    coef = rti.fit(I, lu, lv, kernel=kernel, layout="planar").reshape(6, -1)
+    scale = a_true.abs().amax(0).clamp_min(1.0)
+    assert float(((coef - a_true).abs() / scale).max()) < 1e-4
+    # sampled pixels against the fp64 oracle on the same (fp32) stack
+    idx = torch.randint(0, H * W, (4096,), generator=g, device=cuda)
+    Is = I.reshape(N, -1)[:, idx].cpu().numpy()
+    ref = o.fit_shared(Is, o.pinv_shared("ptm", lu, lv))
+    err, ok = coef_close(coef[:, idx].T.cpu().numpy(), ref)
+    assert ok, err
+    # linearity: fit(2I + 3) = 2 fit(I) + fit(3)
+    coef2 = rti.fit(2 * I + 3, lu, lv, kernel=kernel, layout="planar").reshape(6, -1)
+    c3 = torch.as_tensor(o.pinv_shared("ptm", lu, lv).sum(1) * 3, device=cuda, dtype=torch.float32)[:, None]
+    assert float(((coef2 - 2 * coef - c3).abs() / (2 * scale)).max()) < 1e-4
