@@ -337,11 +337,11 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     use_mfma = false;
   else
     use_mfma = !valu_k || k == 16;
-  const bool mfma_ok = N <= 2048 && P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 &&
+  const bool mfma_ok = N <= 1024 && P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 &&
                        aligned_to(I, 4 * es) && aligned_to(coef, 16) && a.ocstride % 4 == 0;
   if (use_mfma && !mfma_ok) {
     if (sel == RTI_KERNEL_MFMA && !valu_k)
-      return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: MFMA path needs N<=2048 and 4-pixel alignment");
+      return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: MFMA path needs N<=1024 and 4-pixel alignment");
     use_mfma = false;
   }
   if (!use_mfma && !valu_k) return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: VALU path supports k in {6,9,16}");
