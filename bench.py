@@ -64,11 +64,14 @@ def synth_stack(H, W, N, C, basis, lu, lv, seed, device):
             s = (torch.sin(2 * np.pi * (f1 + 0.5) * xx + p1) * torch.cos(2 * np.pi * (f2 + 0.5) * yy + p2)).reshape(-1)
             base, amp = (130.0, 70.0) if (basis == "ptm" and j == k - 1) or (basis != "ptm" and j == 0) else (0.0, 50.0)
             a[j] = base + amp * s
-        for n0 in range(0, N, 25):
-            n1 = min(N, n0 + 25)
-            blk = B[n0:n1] @ a
-            blk += torch.randn(blk.shape, generator=g, device=device) * 2.0
-            out[c, n0:n1] = blk.round_().clamp_(0, 255)
+        # element-wise accumulation: torch's fp32 GEMM returns wrong values for
+        # [n,6] @ [6, 8294400] on this ROCm stack (tools/probe_matmul.py), so no library GEMM here
+        Bh = B.cpu().numpy()
+        for n in range(N):
+            row = torch.randn(H * W, generator=g, device=device) * 2.0
+            for j in range(k):
+                row.add_(a[j], alpha=float(Bh[n, j]))
+            out[c, n] = row.round_().clamp_(0, 255)
         del a
     return out
 
@@ -111,7 +114,8 @@ def load_traffic(workload_key):
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(workload_key)
+            entry = json.load(f).get(workload_key) or {}
+        return entry.get("traffic_bytes_per_launch")
     except (OSError, ValueError):
         return None
 

@@ -61,7 +61,11 @@ extern "C" {
 #define RTI_KERNEL_AUTO 0
 #define RTI_KERNEL_VALU 1   /* pinv in SGPRs, fp32 FMA stream */
 #define RTI_KERNEL_MFMA 2   /* v_mfma_f32_16x16x4_f32, pinv staged in LDS */
-#define RTI_KERNEL_NONTEMPORAL 0x100  /* OR-able flag: non-temporal loads of the intensity stream */
+/* OR-able tuning flags (VALU kernel; only NONTEMPORAL applies to the MFMA kernel) */
+#define RTI_KERNEL_NONTEMPORAL 0x100  /* non-temporal intensity loads (the stack is read once) */
+#define RTI_KERNEL_PINV_LDS    0x200  /* stage pinv in LDS instead of scalar loads */
+#define RTI_KERNEL_NT_STORE    0x400  /* non-temporal coefficient stores */
+#define RTI_KERNEL_STAGE       0x800  /* pixel-major output transposed through LDS (1 KiB stores) */
 
 typedef void* rti_stream_t; /* hipStream_t */
 

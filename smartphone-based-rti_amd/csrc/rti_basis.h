@@ -37,6 +37,7 @@ __host__ __device__ inline int basis_terms(int basis) {
 // Hemispherical harmonics, first k terms (k = 9 or 16), type T arithmetic.
 template <typename T>
 __host__ __device__ inline void hsh_eval(T lu, T lv, int k, T* out) {
+#pragma clang fp contract(off)  // identical values in every kernel and on the host
   T r2 = lu * lu + lv * lv;
   T lw2 = T(1) - r2;
   T lw = lw2 > T(0) ? sqrt(lw2) : T(0);
@@ -84,6 +85,7 @@ __host__ __device__ inline void hsh_eval(T lu, T lv, int k, T* out) {
 // lu**2, lv**2, lu*lv in the coefficient precision).
 template <typename T>
 __host__ __device__ inline void ptm_eval(T lu, T lv, T* out) {
+#pragma clang fp contract(off)
   out[0] = lu * lu;
   out[1] = lv * lv;
   out[2] = lu * lv;

@@ -62,10 +62,54 @@ __device__ __forceinline__ void store_f32(float* __restrict__ dst, const float (
 }
 
 // ---- VALU stream kernel ---------------------------------------------------------------
-template <int K, int VEC, typename T, int LAYOUT, bool NT>
+// MODE bits (tuning variants, picked by measurement):
+//   VM_NT    : non-temporal loads of the intensity stream (read once)
+//   VM_LDS   : pinv staged in LDS as [N][KP] (KP = K rounded up to 4), read back with
+//              broadcast LDS loads instead of per-light scalar loads
+//   VM_NTS   : non-temporal coefficient stores
+//   VM_STAGE : pixel-major output transposed through LDS so every store instruction
+//              writes 1 KiB contiguous (a lane's own VEC*K floats sit at a 4*VEC*K-byte
+//              lane stride otherwise)
+constexpr int VM_NT = 1, VM_LDS = 2, VM_NTS = 4, VM_STAGE = 8;
+
+template <int N, bool NT>
+__device__ __forceinline__ void store_f32_nt(float* __restrict__ dst, const float (&v)[N]) {
+  if constexpr (!NT) {
+    store_f32<N>(dst, v);
+  } else if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      floatx4 t = {v[i], v[i + 1], v[i + 2], v[i + 3]};
+      __builtin_nontemporal_store(t, reinterpret_cast<floatx4*>(dst + i));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) __builtin_nontemporal_store(v[i], dst + i);
+  }
+}
+
+template <int K, int VEC>
+constexpr bool stage_ok() { return VEC == 4 && (VEC * K) % 4 == 0 && K <= 9; }
+
+// dynamic LDS: [pinv weights N*KP floats, 16-B aligned][staging 4 waves * 64 lanes * VEC*K floats]
+template <int K, int VEC, typename T, int LAYOUT, int MODE>
 __global__ void __launch_bounds__(256)
 fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P,
                 int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  constexpr bool NT = (MODE & VM_NT) != 0;
+  constexpr bool LDSW = (MODE & VM_LDS) != 0;
+  constexpr bool NTS = (MODE & VM_NTS) != 0;
+  constexpr bool STAGE = (MODE & VM_STAGE) != 0 && LAYOUT == RTI_COEF_PIXEL_MAJOR && stage_ok<K, VEC>();
+  constexpr int KP = (K + 3) & ~3;
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  float* lds_w = lds_dyn;
+  if constexpr (LDSW) {
+    for (int idx = threadIdx.x; idx < N * KP; idx += 256) {
+      const int n = idx / KP, k = idx - n * KP;
+      lds_w[idx] = k < K ? pinv[k * N + n] : 0.f;
+    }
+    __syncthreads();
+  }
   const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
   if (p0 >= P) return;
   const T* __restrict__ src = I + (int64_t)blockIdx.y * cstride + p0;
@@ -76,7 +120,14 @@ fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, 
 #pragma unroll
     for (int v = 0; v < VEC; ++v) acc[k][v] = 0.f;
 
-  constexpr int U = (VEC >= 16) ? 4 : 8;  // loads in flight per lane
+  auto weight = [&](int k, int n) -> float {
+    if constexpr (LDSW)
+      return lds_w[n * KP + k];  // same address in every lane: broadcast
+    else
+      return pinv[k * N + n];  // wave-uniform -> s_load
+  };
+
+  constexpr int U = (VEC >= 16) ? 4 : 8;  // light planes in flight per lane
   int n = 0;
   for (; n + U <= N; n += U) {
     float x[U][VEC];
@@ -86,7 +137,7 @@ fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, 
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const float w = pinv[k * N + n + u];  // wave-uniform -> s_load
+        const float w = weight(k, n + u);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) acc[k][v] = fmaf(w, x[u][v], acc[k][v]);
       }
@@ -96,7 +147,7 @@ fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, 
     load_px<T, VEC, NT>(src + (int64_t)n * lstride, x);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const float w = pinv[k * N + n];
+      const float w = weight(k, n);
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc[k][v] = fmaf(w, x[v], acc[k][v]);
     }
@@ -105,14 +156,39 @@ fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, 
   float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
   if constexpr (LAYOUT == RTI_COEF_PLANAR) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) store_f32<VEC>(dst + (int64_t)k * P + p0, acc[k]);
+    for (int k = 0; k < K; ++k) store_f32_nt<VEC, NTS>(dst + (int64_t)k * P + p0, acc[k]);
   } else {
     float o[VEC * K];
 #pragma unroll
     for (int v = 0; v < VEC; ++v)
 #pragma unroll
       for (int k = 0; k < K; ++k) o[v * K + k] = acc[k][v];
-    store_f32<VEC * K>(dst + p0 * K, o);
+    if constexpr (STAGE) {
+      constexpr int F = VEC * K;  // floats per lane (24 for PTM-6)
+      const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+      const int64_t wp0 = ((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63)) * VEC;  // wave's first pixel
+      if (wp0 + 64 * VEC <= P) {  // wave-uniform: the whole wave's 64*F floats are in range
+        const int woff = LDSW ? ((N * KP + 3) & ~3) : 0;
+        float* st = lds_dyn + woff + wave * 64 * F;
+#pragma unroll
+        for (int i = 0; i < F; i += 4)
+          *reinterpret_cast<floatx4*>(st + lane * F + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float* wdst = dst + wp0 * K;
+#pragma unroll
+        for (int j = 0; j < F / 4; ++j) {
+          const floatx4 t = *reinterpret_cast<const floatx4*>(st + j * 256 + lane * 4);
+          if constexpr (NTS)
+            __builtin_nontemporal_store(t, reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4));
+          else
+            *reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4) = t;
+        }
+        return;
+      }
+    }
+    store_f32_nt<VEC * K, NTS>(dst + p0 * K, o);
   }
 }
 
@@ -217,24 +293,48 @@ struct FitArgs {
   int layout;
   int64_t ocstride;
   bool nt;
+  int mode;  // VALU variant bits (VM_*)
   hipStream_t stream;
 };
 
-template <int K, int VEC, typename T, int LAYOUT, bool NT>
+template <int K, int VEC, typename T, int LAYOUT, int MODE>
 void launch_valu_t(const FitArgs& a) {
   const int64_t groups = (a.P + VEC - 1) / VEC;
   dim3 grid(grid_1d(groups, 256), a.C);
-  hipLaunchKernelGGL((fit_shared_valu<K, VEC, T, LAYOUT, NT>), grid, dim3(256), 0, a.stream, a.pinv, a.N,
+  constexpr int KP = (K + 3) & ~3;
+  size_t lds = (MODE & VM_LDS) ? (((size_t)a.N * KP + 3) & ~(size_t)3) * sizeof(float) : 0;
+  if constexpr ((MODE & VM_STAGE) && LAYOUT == RTI_COEF_PIXEL_MAJOR && stage_ok<K, VEC>())
+    lds += (size_t)4 * 64 * VEC * K * sizeof(float);
+  hipLaunchKernelGGL((fit_shared_valu<K, VEC, T, LAYOUT, MODE>), grid, dim3(256), lds, a.stream, a.pinv, a.N,
                      static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride);
+}
+
+template <int K, int VEC, typename T, int LAYOUT>
+void launch_valu_m(const FitArgs& a) {
+  // every mode for the fp32 16-byte path; the default mode for the others
+  if constexpr (VEC > 1 && std::is_same<T, float>::value) {
+    switch (a.mode & 15) {
+#define RTI_MODE_CASE(m) \
+  case m: launch_valu_t<K, VEC, T, LAYOUT, m>(a); break;
+      RTI_MODE_CASE(0) RTI_MODE_CASE(1) RTI_MODE_CASE(2) RTI_MODE_CASE(3) RTI_MODE_CASE(4) RTI_MODE_CASE(5)
+      RTI_MODE_CASE(6) RTI_MODE_CASE(7) RTI_MODE_CASE(8) RTI_MODE_CASE(9) RTI_MODE_CASE(10) RTI_MODE_CASE(11)
+      RTI_MODE_CASE(12) RTI_MODE_CASE(13) RTI_MODE_CASE(14) RTI_MODE_CASE(15)
+#undef RTI_MODE_CASE
+    }
+  } else {
+    if (a.mode & VM_NT)
+      launch_valu_t<K, VEC, T, LAYOUT, VM_NT>(a);
+    else
+      launch_valu_t<K, VEC, T, LAYOUT, 0>(a);
+  }
 }
 
 template <int K, int VEC, typename T>
 void launch_valu_l(const FitArgs& a) {
   if (a.layout == RTI_COEF_PLANAR)
-    a.nt ? launch_valu_t<K, VEC, T, RTI_COEF_PLANAR, true>(a) : launch_valu_t<K, VEC, T, RTI_COEF_PLANAR, false>(a);
+    launch_valu_m<K, VEC, T, RTI_COEF_PLANAR>(a);
   else
-    a.nt ? launch_valu_t<K, VEC, T, RTI_COEF_PIXEL_MAJOR, true>(a)
-         : launch_valu_t<K, VEC, T, RTI_COEF_PIXEL_MAJOR, false>(a);
+    launch_valu_m<K, VEC, T, RTI_COEF_PIXEL_MAJOR>(a);
 }
 
 template <int K, typename T>
@@ -316,6 +416,9 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
   a.layout = coef_layout;
   a.ocstride = coef_channel_stride ? coef_channel_stride : P * k;
   a.nt = (kernel & RTI_KERNEL_NONTEMPORAL) != 0;
+  a.mode = (a.nt ? VM_NT : 0) | ((kernel & RTI_KERNEL_PINV_LDS) ? VM_LDS : 0) |
+           ((kernel & RTI_KERNEL_NT_STORE) ? VM_NTS : 0) | ((kernel & RTI_KERNEL_STAGE) ? VM_STAGE : 0);
+  if ((a.mode & VM_LDS) && (size_t)N * 16 * sizeof(float) > 24576) a.mode &= ~VM_LDS;  // keep LDS <= 64 KiB
   a.stream = (hipStream_t)stream;
   if (a.lstride < P) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: light_stride < P");
   if (C > 1 && a.cstride < (int64_t)N * a.lstride) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: channel_stride");
@@ -331,12 +434,17 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
   const int sel = kernel & 0xff;
   const bool valu_k = (k == 6 || k == 9 || k == 16);
   bool use_mfma;
-  if (sel == RTI_KERNEL_MFMA)
+  if (sel == RTI_KERNEL_MFMA) {
     use_mfma = true;
-  else if (sel == RTI_KERNEL_VALU)
+  } else if (sel == RTI_KERNEL_VALU) {
     use_mfma = false;
-  else
-    use_mfma = !valu_k || k == 16;
+  } else {
+    // AUTO: measured best on MI355X (profiles/): the VALU stream with
+    // non-temporal intensity loads, SGPR weights and plain coefficient stores.
+    use_mfma = !valu_k;
+    a.nt = true;
+    a.mode = VM_NT;
+  }
   const bool mfma_ok = N <= 1024 && P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 &&
                        aligned_to(I, 4 * es) && aligned_to(coef, 16) && a.ocstride % 4 == 0;
   if (use_mfma && !mfma_ok) {

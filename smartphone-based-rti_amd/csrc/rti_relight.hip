@@ -32,14 +32,6 @@ namespace {
 constexpr int ECH = 64;  // evals per eval-major block (basis table in LDS)
 
 template <typename TC>
-__device__ __forceinline__ TC madd(TC acc, TC c, TC b) {
-  if constexpr (std::is_same<TC, double>::value)
-    return __dadd_rn(acc, __dmul_rn(c, b));  // no contraction: reference op order
-  else
-    return fmaf(c, b, acc);
-}
-
-template <typename TC>
 __device__ __forceinline__ int32_t trunc_i32(TC v) {
   // C truncation toward zero; NaN / out of range -> INT32_MIN (x86 cvttsd2si,
   // which is what NumPy's float64 -> int32 element assignment produces).
@@ -57,11 +49,22 @@ __device__ __forceinline__ TO cvt_out(TC v) {
   }
 }
 
-template <int K, typename TC>
-__device__ __forceinline__ TC dot_k(const TC (&c)[K], const TC* b) {
-  TC acc = c[0] * b[0];
+// fp64: the reference's order, every product and sum rounded (analysis.py:307-312).
+template <int K>
+__device__ __forceinline__ double dot_k(const double (&c)[K], const double* b) {
+#pragma clang fp contract(off)
+  double acc = c[0] * b[0];
 #pragma unroll
-  for (int k = 1; k < K; ++k) acc = madd(acc, c[k], b[k]);
+  for (int k = 1; k < K; ++k) acc = acc + c[k] * b[k];
+  return acc;
+}
+
+// fp32: fused multiply-adds in the same order.
+template <int K>
+__device__ __forceinline__ float dot_k(const float (&c)[K], const float* b) {
+  float acc = c[0] * b[0];
+#pragma unroll
+  for (int k = 1; k < K; ++k) acc = fmaf(c[k], b[k], acc);
   return acc;
 }
 

@@ -38,6 +38,9 @@ RTI_KERNEL_AUTO = 0
 RTI_KERNEL_VALU = 1
 RTI_KERNEL_MFMA = 2
 RTI_KERNEL_NONTEMPORAL = 0x100
+RTI_KERNEL_PINV_LDS = 0x200
+RTI_KERNEL_NT_STORE = 0x400
+RTI_KERNEL_STAGE = 0x800
 
 
 class RTILibraryMissing(ImportError):

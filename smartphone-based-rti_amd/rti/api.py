@@ -117,7 +117,7 @@ def _layout_id(layout):
     raise ValueError(f"unknown coefficient layout {layout!r} (expected 'pixel' or 'planar')")
 
 
-def fit_shared_into(pinv_dev, I, coef, *, k, layout="pixel", kernel="auto", nontemporal=False):
+def fit_shared_into(pinv_dev, I, coef, *, k, layout="pixel", kernel="auto", nontemporal=False, flags=0):
     """Launch ``rti_fit_shared`` on preallocated tensors (no allocation, graph-capturable).
 
     pinv_dev: CUDA fp32 [k, N]; I: CUDA [C, N, P] or [N, P] (contiguous
@@ -129,6 +129,7 @@ def fit_shared_into(pinv_dev, I, coef, *, k, layout="pixel", kernel="auto", nont
     kern = _KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
     if nontemporal:
         kern |= L.RTI_KERNEL_NONTEMPORAL
+    kern |= int(flags)
     st = L.lib().rti_fit_shared(_vp(pinv_dev), k, N, _vp(I), _IN_DTYPES[I.dtype], P, C, P, N * P, _vp(coef),
                                 _layout_id(layout), P * k, kern, _stream_of(I))
     L.check(st, "rti_fit_shared")

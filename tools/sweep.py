@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of fit-kernel variants in ONE process (methodology
+rule 24): every round runs each variant once, HIP events around each launch;
+reports median / min kernel time and GB/s (algorithmic bytes) per variant,
+plus the pure read-stream ceiling from tools/probe/libhbm_probe.so.
+
+  python tools/sweep.py [--config c3] [--rounds 30]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "smartphone-based-rti_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import rti  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--rounds", type=int, default=30)
+    ap.add_argument("--variants", default="valu:pixel,valu:pixel:nt,valu:pixel:nt+lds,valu:pixel:nt+stage,"
+                    "valu:pixel:nt+lds+stage,valu:pixel:nt+stage+nts,valu:pixel:nt+lds+stage+nts,"
+                    "valu:planar:nt,valu:planar:nt+nts,valu:planar:nt+lds+nts,valu:planar:nt+lds,"
+                    "mfma:planar:nt,mfma:pixel:nt")
+    ap.add_argument("--no-probe", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    H, W, N, C, basis, desc = bench.CONFIGS[args.config]
+    k = rti.basis_terms(basis)
+    P = H * W
+    lu, lv = bench.synth_dirs(N, 2)
+    I = bench.synth_stack(H, W, N, C, basis, lu, lv, 1000, dev)
+    pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=dev)
+    coefs = {"pixel": torch.empty((C, P, k), device=dev), "planar": torch.empty((C, k, P), device=dev)}
+    variants = []
+    for v in args.variants.split(","):
+        parts = v.split(":")
+        opts = parts[2].split("+") if len(parts) > 2 else []
+        fl = (rti._lib.RTI_KERNEL_NONTEMPORAL if "nt" in opts else 0) | \
+             (rti._lib.RTI_KERNEL_PINV_LDS if "lds" in opts else 0) | \
+             (rti._lib.RTI_KERNEL_NT_STORE if "nts" in opts else 0) | (rti._lib.RTI_KERNEL_STAGE if "stage" in opts else 0)
+        variants.append((v, parts[0], parts[1], fl))
+    probe = None
+    plib = os.path.join(ROOT, "tools", "probe", "libhbm_probe.so")
+    if os.path.exists(plib) and C == 1 and not args.no_probe:
+        probe = ctypes.CDLL(plib)
+        probe.probe_read.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.c_void_p]
+        sink = torch.zeros(1, device=dev)
+        for pvnt in (0, 1, 2, 3):
+            variants.append((f"probe_read_v{pvnt}", "probe", str(pvnt), 0))
+    stream = torch.cuda.current_stream(dev)
+    times = {name: [] for name, *_ in variants}
+
+    def launch(kern, layout, fl):
+        if kern == "probe":
+            probe.probe_read(ctypes.c_void_p(I.data_ptr()), N, P, ctypes.c_void_p(sink.data_ptr()), int(layout),
+                             ctypes.c_void_p(stream.cuda_stream))
+        else:
+            rti.fit_shared_into(pv, I, coefs[layout], k=k, layout=layout, kernel=kern, flags=fl)
+
+    for name, kern, layout, fl in variants:  # warm-up
+        for _ in range(3):
+            launch(kern, layout, fl)
+    torch.cuda.synchronize()
+    for _ in range(args.rounds):
+        for name, kern, layout, fl in variants:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            launch(kern, layout, fl)
+            b.record(stream)
+            times[name].append((a, b))
+    torch.cuda.synchronize()
+    alg = 4.0 * P * N * C + 4.0 * P * k * C
+    res = {}
+    for name, *rest in variants:
+        ms = np.array([a.elapsed_time(b) for a, b in times[name]])
+        byts = 4.0 * P * N if name.startswith("probe") else alg
+        res[name] = {"median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
+                     "GBps_median": byts / (np.median(ms) * 1e-3) / 1e9}
+        print(f"{name:24s} median {np.median(ms):.4f} ms  min {ms.min():.4f} ms  "
+              f"{res[name]['GBps_median']:.0f} GB/s ({res[name]['GBps_median'] / 80:.1f}% of 8 TB/s)", flush=True)
+    print(json.dumps({"config": args.config, "results": res}))
+
+
+if __name__ == "__main__":
+    main()
