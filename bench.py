@@ -32,10 +32,14 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 CONFIGS = {
-    # name: (H, W, lights, channels, basis, description)
-    "c2": (1080, 1920, 50, 1, "ptm", "ptm6-fit 1920x1080 N=50 fp32 (BASELINE configs[1])"),
-    "c3": (2160, 3840, 100, 1, "ptm", "ptm6-fit 3840x2160 N=100 fp32 (BASELINE configs[2], metric config)"),
-    "c4": (2160, 3840, 200, 3, "hsh", "hsh16-fit 3840x2160 RGB N=200 fp32 (BASELINE configs[3])"),
+    # name: (kind, H, W, lights/evals, channels, basis, description)
+    "c2": ("fit", 1080, 1920, 50, 1, "ptm", "ptm6-fit 1920x1080 N=50 fp32 (BASELINE configs[1])"),
+    "c3": ("fit", 2160, 3840, 100, 1, "ptm", "ptm6-fit 3840x2160 N=100 fp32 (BASELINE configs[2], metric config)"),
+    "c4": ("fit", 2160, 3840, 200, 3, "hsh", "hsh16-fit 3840x2160 RGB N=200 fp32 (BASELINE configs[3])"),
+    "c5": ("relight", 2160, 3840, 1000, 1, "ptm",
+           "ptm6-relight 3840x2160, 1000 random (lu,lv) streamed one per launch, fp32 out (BASELINE configs[4])"),
+    "c6": ("perpixel", 2160, 3840, 100, 1, "ptm",
+           "ptm6 per-pixel fit 3840x2160 N=100, light vectors from camera positions in-kernel (reference geometry)"),
 }
 
 
@@ -76,40 +80,6 @@ def synth_stack(H, W, N, C, basis, lu, lv, seed, device):
     return out
 
 
-def cpu_baseline(I_dev, pinv64, N, W, budget_s=10.0):
-    """Oracle restatement: fp64 pinv (already built) + fp32 matmul on (N, P) light-major rows."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import rti_oracle as o
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([t.get("num_threads", 1) for t in threadpool_info() if t.get("user_api") == "blas"] or [1])
-    except Exception:  # pragma: no cover
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    rows = 216  # a tenth of a 4K frame, all N lights
-    sample = I_dev[0, :, : rows * W].cpu().numpy()  # [N, rows*W]
-    units = N * rows * W
-    o.fit_shared_f32(sample, pinv64)  # warm-up
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        o.fit_shared_f32(sample, pinv64)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    cpu_name = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_name = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": units * reps / el / 1e6, "unit": "Mpix*lights/s", "cores": int(threads), "kind": "port",
-            "sample": f"oracle fit_shared_f32 (fp64 pinv + fp32 numpy matmul) on {rows}x{W} px x {N} lights, "
-                      f"{reps} reps in {el:.1f}s; {cpu_name}"}
-
-
 def load_traffic(workload_key):
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
@@ -120,10 +90,204 @@ def load_traffic(workload_key):
         return None
 
 
+def synth_cams(n, seed, H, W):
+    """Camera positions on a hemisphere above the image centre (ROI pixel units, analysis.py:228)."""
+    rng = np.random.default_rng(seed)
+    th = np.arccos(rng.uniform(0.35, 0.95, n))
+    ph = rng.uniform(0, 2 * np.pi, n)
+    rad = rng.uniform(1.5, 2.5, n) * max(H, W)
+    return np.stack([W / 2 + rad * np.sin(th) * np.cos(ph), H / 2 + rad * np.sin(th) * np.sin(ph),
+                     rad * np.cos(th)], -1)
+
+
+def cpu_sample_rate(fn, units, budget_s):
+    fn()  # warm-up
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        fn()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            return units * reps / el / 1e6, reps, el
+
+
+def cpu_info():
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([t.get("num_threads", 1) for t in threadpool_info() if t.get("user_api") == "blas"] or [1])
+    except Exception:  # pragma: no cover
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    name = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                name = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return int(threads), name
+
+
+class FitWorkload:
+    """One step = one rti_fit_shared launch over the rank's whole stack."""
+
+    def __init__(self, args, cfg, rank, dev):
+        import rti
+
+        self.rti = rti
+        _, H, W, N, C, basis, desc = cfg
+        self.H, self.W, self.N, self.C, self.basis, self.desc = H, W, N, C, basis, desc
+        self.k = k = rti.basis_terms(basis)
+        self.P = P = H * W
+        self.args = args
+        self.lu, self.lv = synth_dirs(N, seed=2)
+        self.I = synth_stack(H, W, N, C, basis, self.lu, self.lv, seed=1000 + rank, device=dev)
+        self.pinv64 = rti.pinv(self.lu, self.lv, basis)
+        self.pinv_dev = torch.as_tensor(self.pinv64.astype(np.float32), device=dev)
+        self.coef = torch.empty((C, P, k) if args.layout == "pixel" else (C, k, P), dtype=torch.float32, device=dev)
+        self.units = P * N * C
+        self.alg_bytes = 4.0 * P * N * C + 4.0 * P * k * C  # fp32 stack read once + fp32 coefficients written
+        self.metric = "Mpix*lights/sec PTM fit (4K, 100 lights)" if args.config == "c3" else f"Mpix*lights/sec {desc}"
+        self.unit = "Mpix*lights/s"
+
+    def step(self, i):
+        self.rti.fit_shared_into(self.pinv_dev, self.I, self.coef, k=self.k, layout=self.args.layout,
+                                 kernel=self.args.kernel, nontemporal=self.args.nontemporal)
+
+    def config(self):
+        return {"lights": self.N, "channels": self.C, "basis": self.basis, "k": self.k,
+                "coef_layout": self.args.layout, "kernel": self.args.kernel}
+
+    def cpu_baseline(self, budget_s):
+        """Oracle restatement: fp64 pinv + fp32 NumPy matmul on light-major rows."""
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import rti_oracle as o
+
+        rows = max(1, self.H // 10)
+        sample = self.I[0, :, : rows * self.W].cpu().numpy()
+        rate, reps, el = cpu_sample_rate(lambda: o.fit_shared_f32(sample, self.pinv64), self.N * rows * self.W,
+                                         budget_s)
+        threads, name = cpu_info()
+        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oracle fit_shared_f32 (fp64 pinv + fp32 NumPy matmul, channel 0) on {rows}x{self.W} px "
+                          f"x {self.N} lights, {reps} reps in {el:.1f}s; {name}"}
+
+
+class RelightWorkload:
+    """One step = one rti_relight launch evaluating ONE (lu, lv) over the 4K coefficient maps (interactive)."""
+
+    def __init__(self, args, cfg, rank, dev):
+        import rti
+
+        self.rti = rti
+        _, H, W, E, C, basis, desc = cfg
+        self.H, self.W, self.E, self.desc, self.basis = H, W, E, desc, basis
+        self.k = k = rti.basis_terms(basis)
+        self.P = P = H * W
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        self.coef = (torch.rand((P, k), generator=g, device=dev) * 100 - 50).contiguous()
+        self.coef[:, k - 1] += 130
+        rng = np.random.default_rng(4)
+        r = np.sqrt(rng.random(E))
+        th = 2 * np.pi * rng.random(E)
+        self.luv = torch.as_tensor(np.stack([r * np.cos(th), r * np.sin(th)], -1), device=dev).contiguous()
+        self.out = torch.empty((P,), dtype=torch.float32, device=dev)
+        self.units = P
+        self.alg_bytes = 4.0 * P * k + 4.0 * P  # coefficients read + fp32 image written, per eval
+        self.metric = f"Mpix*evals/sec {desc}"
+        self.unit = "Mpix*evals/s"
+        import ctypes
+
+        self.ctypes = ctypes
+        self.lib = rti._lib.lib()
+        self.bid = rti.basis_id(basis)
+
+    def step(self, i):
+        c = self.ctypes
+        e = i % self.E
+        st = self.lib.rti_relight(c.c_void_p(self.coef.data_ptr()), self.rti._lib.RTI_F32, self.bid, self.P,
+                                  self.rti._lib.RTI_COEF_PIXEL_MAJOR, c.c_void_p(self.luv.data_ptr() + 16 * e), 1,
+                                  c.c_void_p(self.out.data_ptr()), self.rti._lib.RTI_F32,
+                                  self.rti._lib.RTI_OUT_EVAL_MAJOR,
+                                  c.c_void_p(torch.cuda.current_stream().cuda_stream))
+        self.rti._lib.check(st, "rti_relight")
+
+    def config(self):
+        return {"evals": self.E, "basis": self.basis, "k": self.k, "coef_layout": "pixel", "out": "f32"}
+
+    def cpu_baseline(self, budget_s):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import rti_oracle as o
+
+        rows = max(1, self.H // 10)
+        c = self.coef[: rows * self.W].cpu().numpy()
+        lu, lv = self.luv[0].cpu().numpy()
+        rate, reps, el = cpu_sample_rate(lambda: o.relight(c, self.basis, lu, lv), rows * self.W, budget_s)
+        threads, name = cpu_info()
+        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oracle relight (fp64 NumPy) on {rows}x{self.W} px x 1 eval, {reps} reps in {el:.1f}s; "
+                          f"{name}"}
+
+
+class PerPixelWorkload:
+    """One step = one rti_fit_perpixel_cam launch (directions from cameras, fp64 normal equations)."""
+
+    def __init__(self, args, cfg, rank, dev):
+        import rti
+
+        self.rti = rti
+        _, H, W, N, C, basis, desc = cfg
+        self.H, self.W, self.N, self.desc = H, W, N, desc
+        self.P = P = H * W
+        self.cams = synth_cams(N, 6, H, W)
+        lu, lv = synth_dirs(N, seed=2)
+        self.I = synth_stack(H, W, N, 1, "ptm", lu, lv, seed=1000 + rank, device=dev)[0]  # [N, P]
+        self.cams_d = torch.as_tensor(self.cams, device=dev).contiguous()
+        self.coef = torch.empty((P, 6), dtype=torch.float32, device=dev)
+        self.units = P * N
+        self.alg_bytes = 4.0 * P * N + 4.0 * P * 6
+        self.metric = f"Mpix*lights/sec {desc}"
+        self.unit = "Mpix*lights/s"
+        import ctypes
+
+        self.ctypes = ctypes
+        self.lib = rti._lib.lib()
+
+    def step(self, i):
+        c = self.ctypes
+        L = self.rti._lib
+        st = self.lib.rti_fit_perpixel_cam(c.c_void_p(self.cams_d.data_ptr()), self.N, c.c_void_p(self.I.data_ptr()),
+                                           L.RTI_F32, self.H, self.W, self.P, 0.0, 0.0, -1.0,
+                                           c.c_void_p(self.coef.data_ptr()), L.RTI_F32, L.RTI_COEF_PIXEL_MAJOR,
+                                           c.c_void_p(torch.cuda.current_stream().cuda_stream))
+        L.check(st, "rti_fit_perpixel_cam")
+
+    def config(self):
+        return {"lights": self.N, "basis": "ptm", "k": 6, "coef_layout": "pixel", "geometry": "per-pixel cameras"}
+
+    def cpu_baseline(self, budget_s):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import rti_oracle as o
+
+        npx = 4096
+        ys, xs = np.divmod(np.arange(npx), self.W)
+        lu, lv = o.light_dirs_for_pixels(self.cams, xs, ys)
+        I = self.I[:, :npx].cpu().numpy().T
+        rate, reps, el = cpu_sample_rate(lambda: o.fit_perpixel(lu, lv, I), npx * self.N, budget_s)
+        threads, name = cpu_info()
+        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oracle fit_perpixel (batched fp64 NumPy SVD, reference semantics) on {npx} px x "
+                          f"{self.N} lights, {reps} reps in {el:.1f}s; {name}"}
+
+
+WORKLOADS = {"fit": FitWorkload, "relight": RelightWorkload, "perpixel": PerPixelWorkload}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="default 20 (fit) / 1000 (relight) / 10 (per-pixel)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma"])
@@ -132,63 +296,69 @@ def main():
     ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of the maps")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) for real runs; gloo lets ranks share one GPU in rehearsals")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    kind = cfg[0]
+    if args.steps is None:
+        args.steps = {"fit": 20, "relight": 1000, "perpixel": 10}[kind]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", local % ndev)
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     import rti
 
     rti.load()
-    H, W, N, C, basis, desc = CONFIGS[args.config]
-    k = rti.basis_terms(basis)
-    P = H * W
-    lu, lv = synth_dirs(N, seed=2)
-    I = synth_stack(H, W, N, C, basis, lu, lv, seed=1000 + rank, device=dev)  # this rank's stripe
-    pinv64 = rti.pinv(lu, lv, basis)
-    pinv_dev = torch.as_tensor(pinv64.astype(np.float32), device=dev)
-    shape = (C, P, k) if args.layout == "pixel" else (C, k, P)
-    coef = torch.empty(shape, dtype=torch.float32, device=dev)
+    wl = WORKLOADS[kind](args, cfg, rank, dev)
     torch.cuda.synchronize(dev)
 
-    def step():
-        rti.fit_shared_into(pinv_dev, I, coef, k=k, layout=args.layout, kernel=args.kernel,
-                            nontemporal=args.nontemporal)
-
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        wl.step(i)
     torch.cuda.synchronize(dev)
 
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # timed region: exactly K steps between barrier + synchronize, nothing else enqueued
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
+        wl.step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    # kernel duration for the roofline: HIP events around each launch, on the launch stream,
+    # in a separate pass so the events do not add gaps to the timed region
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        wl.step(i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
 
     gather_ms = None
-    if args.allgather and world > 1:
+    if args.allgather and world > 1 and kind == "fit":
         from rti.parallel import gather_rows
 
-        local_map = coef[0].reshape(H, W, k) if args.layout == "pixel" else coef[0].reshape(k, H, W)
+        H, W, k = wl.H, wl.W, wl.k
+        local_map = wl.coef[0].reshape(H, W, k) if args.layout == "pixel" else wl.coef[0].reshape(k, H, W)
         for _ in range(2):
             gather_rows(local_map, H * world)
         torch.cuda.synchronize(dev)
@@ -199,19 +369,20 @@ def main():
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) / 5 * 1e3
 
-    units_per_rank = P * N * C  # pixel·lights(·channels) per step
-    value = world * units_per_rank * args.steps / elapsed / 1e6
-    alg_bytes = 4.0 * P * N * C + 4.0 * P * k * C  # fp32 intensities read + fp32 coefficients written
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    value = world * wl.units * args.steps / elapsed / 1e6
+    achieved = wl.alg_bytes / (kernel_ms * 1e-3) / 1e9
     workload_key = f"{args.config}-{args.kernel}-{args.layout}"
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(I, pinv64, N, W, budget_s=args.cpu_budget)
+        cpu = wl.cpu_baseline(args.cpu_budget)
     if rank == 0:
+        conf = {"workload": wl.desc, "H_per_rank": wl.H, "W": wl.W}
+        conf.update(wl.config())
+        conf["parallelism"] = f"row-stripes x{world} (one {wl.H}-row stripe per GPU)"
         line = {
-            "metric": "Mpix*lights/sec PTM fit (4K, 100 lights)" if args.config == "c3" else f"Mpix*lights/sec {desc}",
+            "metric": wl.metric,
             "value": round(value, 1),
-            "unit": "Mpix*lights/s",
+            "unit": wl.unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -219,14 +390,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if kind != "perpixel" else "f32 in / f64 solve",
             "data": "synthetic (seeded smooth PTM/HSH coefficient fields + N(0,2) noise, rounded to 0..255, fp32)",
-            "config": {"workload": desc, "H_per_rank": H, "W": W, "lights": N, "channels": C, "basis": basis,
-                       "k": k, "coef_layout": args.layout, "kernel": args.kernel,
-                       "parallelism": f"row-stripes x{world} (one {H}-row stripe per GPU)"},
+            "config": conf,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(workload_key),
-                         "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": alg_bytes},
+                         "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": wl.alg_bytes},
             "cpu_baseline": cpu,
         }
         if gather_ms is not None:

@@ -35,9 +35,11 @@ def gather_rows(local, H, group=None):
         full = torch.empty((world * hmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(full, pad, group=group)
         parts = full.split(hmax)
-    else:
-        parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad, group=group)
+    else:  # gloo: host tensors
+        host = pad.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        parts = [p.to(local.device) for p in parts]
     return torch.cat([p[: r1 - r0] for p, (r0, r1) in zip(parts, rows)], dim=0)
 
 

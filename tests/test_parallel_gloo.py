@@ -1,0 +1,68 @@
+"""Row-block sharding + coefficient-map all-gather (rti.parallel) with world_size 2
+over gloo on the CPU.  The GPU path uses the same code with backend "nccl" (RCCL)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from rti.parallel import gather_rows, row_range
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("H,world", [(2160, 8), (7, 3), (5, 8), (1, 2), (270, 4)])
+def test_row_range_partitions_rows(H, world):
+    ranges = [row_range(H, world, r) for r in range(world)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == H
+    for (a0, a1), (b0, b1) in zip(ranges, ranges[1:]):
+        assert a1 == b0
+    sizes = [r1 - r0 for r0, r1 in ranges]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def _worker(rank, world, port, H, W, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+        import rti_oracle as o
+
+        lu, lv = o.synth_dirs(20, 1)
+        I = o.synth_intensities(H, W, lu, lv, seed=4)  # every rank holds the same image, fits its rows
+        pv = o.pinv_shared("ptm", lu, lv)
+        r0, r1 = row_range(H, world, rank)
+        local = torch.as_tensor(o.fit_shared(I[:, r0:r1], pv).reshape(r1 - r0, W, 6))
+        full = gather_rows(local, H)
+        # the gathered map must be exactly the row blocks every rank fitted, in row order
+        ref = np.concatenate([o.fit_shared(I[:, a:b], pv).reshape(b - a, W, 6)
+                              for a, b in (row_range(H, world, r) for r in range(world))])
+        q.put((rank, bool(np.array_equal(full.numpy(), ref)), tuple(full.shape)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("H,W", [(9, 5), (16, 8)])
+def test_gather_rows_two_ranks(H, W):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, shape in results:
+        assert ok and shape == (H, W, 6), (rank, shape)

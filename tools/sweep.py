@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--no-probe", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    H, W, N, C, basis, desc = bench.CONFIGS[args.config]
+    _, H, W, N, C, basis, desc = bench.CONFIGS[args.config]
     k = rti.basis_terms(basis)
     P = H * W
     lu, lv = bench.synth_dirs(N, 2)
