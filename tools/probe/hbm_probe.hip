@@ -1,12 +1,18 @@
 // hbm_probe.hip -- measurement-only kernels (not part of librti): the achievable
-// HBM read ceiling for a light-major stream, to price the fit kernels against.
+// HBM read ceiling for a light-major stream, and fit-shaped variants that isolate
+// what the PTM fit adds on top of the pure read (stores, weights, loop shape).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// Each lane reads 16 B per "light" plane, UNROLL planes in flight, like the fit kernel,
-// but does one add per element instead of the contraction.
+template <bool NT>
+__device__ __forceinline__ floatx4 ld4(const float* p) {
+  const floatx4* q = reinterpret_cast<const floatx4*>(p);
+  return NT ? __builtin_nontemporal_load(q) : *q;
+}
+
+// Pure read: each lane reads 16 B per light plane, UNROLL planes in flight.
 template <int UNROLL, bool NT>
 __global__ void __launch_bounds__(256) read_stream(const float* __restrict__ I, int N, int64_t P, float* __restrict__ out) {
   const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
@@ -16,15 +22,155 @@ __global__ void __launch_bounds__(256) read_stream(const float* __restrict__ I, 
   for (; n + UNROLL <= N; n += UNROLL) {
     floatx4 x[UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const floatx4* p = reinterpret_cast<const floatx4*>(I + (int64_t)(n + u) * P + p0);
-      x[u] = NT ? __builtin_nontemporal_load(p) : *p;
-    }
+    for (int u = 0; u < UNROLL; ++u) x[u] = ld4<NT>(I + (int64_t)(n + u) * P + p0);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) acc += x[u];
   }
-  for (; n < N; ++n) acc += *reinterpret_cast<const floatx4*>(I + (int64_t)n * P + p0);
+  for (; n < N; ++n) acc += ld4<NT>(I + (int64_t)n * P + p0);
   if (acc[0] + acc[1] + acc[2] + acc[3] == -1.2345f) out[0] = acc[0];  // keep the loads alive
+}
+
+// Fit-shaped: 6 coefficients, weights from global (scalar loads), optional stores,
+// optional software pipelining (next 8 planes issued before this block's FMAs).
+template <bool STORE, bool PIPE>
+__global__ void __launch_bounds__(256) fit6(const float* __restrict__ pinv, const float* __restrict__ I, int N, int64_t P,
+                                            float* __restrict__ coef) {
+  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (p0 >= P) return;
+  float acc[6][4] = {};
+  constexpr int U = 8;
+  const float* src = I + p0;
+  auto fma_block = [&](const floatx4 (&x)[U], int n) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const float w = pinv[k * N + n + u];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[k][v] = fmaf(w, x[u][v], acc[k][v]);
+      }
+  };
+  int n = 0;
+  if constexpr (PIPE) {
+    floatx4 x[U], y[U];
+    if (N >= U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = ld4<true>(src + (int64_t)u * P);
+      for (n = U; n + U <= N; n += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) y[u] = ld4<true>(src + (int64_t)(n + u) * P);
+        fma_block(x, n - U);
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = y[u];
+      }
+      fma_block(x, n - U);
+    }
+  } else {
+    for (; n + U <= N; n += U) {
+      floatx4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = ld4<true>(src + (int64_t)(n + u) * P);
+      fma_block(x, n);
+    }
+  }
+  for (; n < N; ++n) {
+    floatx4 x = ld4<true>(src + (int64_t)n * P);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[k][v] = fmaf(pinv[k * N + n], x[v], acc[k][v]);
+  }
+  if constexpr (STORE) {
+    float o[24];
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) o[v * 6 + k] = acc[k][v];
+    float* d = coef + p0 * 6;
+#pragma unroll
+    for (int i = 0; i < 24; i += 4) *reinterpret_cast<floatx4*>(d + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
+  } else {
+    float s = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+    if (s == -1.2345f) coef[0] = s;
+  }
+}
+
+// Store-path diagnosis: fit6 body (NT loads, no pipelining) with different coefficient stores.
+//   0 plain float4 pixel-major   1 sc1 (write-through, drop from L2) buffer stores   2 sc0|sc1
+//   3 nt buffer stores           4 all waves store into one 64 KiB window (L2-resident)
+//   5 planar float4 (1 KiB contiguous per wave instruction)   6 dword stores pixel-major
+template <int SM>
+__global__ void __launch_bounds__(256) fit6_store(const float* __restrict__ pinv, const float* __restrict__ I, int N,
+                                                  int64_t P, float* __restrict__ coef) {
+  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (p0 >= P) return;
+  float acc[6][4] = {};
+  const float* src = I + p0;
+  int n = 0;
+  for (; n + 8 <= N; n += 8) {
+    floatx4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = ld4<true>(src + (int64_t)(n + u) * P);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const float w = pinv[k * N + n + u];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[k][v] = fmaf(w, x[u][v], acc[k][v]);
+      }
+  }
+  for (; n < N; ++n) {
+    floatx4 x = ld4<true>(src + (int64_t)n * P);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[k][v] = fmaf(pinv[k * N + n], x[v], acc[k][v]);
+  }
+  float o[24];
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o[v * 6 + k] = acc[k][v];
+  if constexpr (SM == 5) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      *reinterpret_cast<floatx4*>(coef + (int64_t)k * P + p0) = floatx4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
+  } else if constexpr (SM == 6) {
+#pragma unroll
+    for (int i = 0; i < 24; ++i) coef[p0 * 6 + i] = o[i];
+  } else if constexpr (SM == 0 || SM == 4) {
+    float* d = SM == 0 ? coef + p0 * 6 : coef + ((p0 * 6) & 16383);
+#pragma unroll
+    for (int i = 0; i < 24; i += 4) *reinterpret_cast<floatx4*>(d + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
+  } else {
+    constexpr int aux = SM == 1 ? 16 : (SM == 2 ? 17 : 2);
+    const int64_t base_f = (int64_t)blockIdx.x * 256 * 24;  // block base (floats), 32-bit voffset inside
+    auto rsrc = __builtin_amdgcn_make_buffer_rsrc(coef + base_f, (short)0, 256 * 24 * 4, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 24; i += 4) {
+      typedef int intx4 __attribute__((ext_vector_type(4)));
+      floatx4 f = {o[i], o[i + 1], o[i + 2], o[i + 3]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(intx4, f), rsrc, (int)(threadIdx.x * 96 + i * 4), 0, aux);
+    }
+  }
+}
+
+extern "C" int probe_store(const float* pinv, const float* I, int N, int64_t P, float* coef, int variant, void* stream) {
+  dim3 grid((unsigned)((P / 4 + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((fit6_store<0>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 1: hipLaunchKernelGGL((fit6_store<1>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 2: hipLaunchKernelGGL((fit6_store<2>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 3: hipLaunchKernelGGL((fit6_store<3>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 4: hipLaunchKernelGGL((fit6_store<4>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 5: hipLaunchKernelGGL((fit6_store<5>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    default: hipLaunchKernelGGL((fit6_store<6>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 extern "C" int probe_read(const float* I, int N, int64_t P, float* out, int variant, void* stream) {
@@ -34,7 +180,21 @@ extern "C" int probe_read(const float* I, int N, int64_t P, float* out, int vari
     case 0: hipLaunchKernelGGL((read_stream<8, false>), grid, dim3(256), 0, s, I, N, P, out); break;
     case 1: hipLaunchKernelGGL((read_stream<8, true>), grid, dim3(256), 0, s, I, N, P, out); break;
     case 2: hipLaunchKernelGGL((read_stream<16, false>), grid, dim3(256), 0, s, I, N, P, out); break;
-    default: hipLaunchKernelGGL((read_stream<4, false>), grid, dim3(256), 0, s, I, N, P, out); break;
+    case 3: hipLaunchKernelGGL((read_stream<16, true>), grid, dim3(256), 0, s, I, N, P, out); break;
+    default: hipLaunchKernelGGL((read_stream<4, true>), grid, dim3(256), 0, s, I, N, P, out); break;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// variant: 0 = stores + no pipelining, 1 = no stores, 2 = stores + pipelined, 3 = no stores + pipelined
+extern "C" int probe_fit6(const float* pinv, const float* I, int N, int64_t P, float* coef, int variant, void* stream) {
+  dim3 grid((unsigned)((P / 4 + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((fit6<true, false>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 1: hipLaunchKernelGGL((fit6<false, false>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 2: hipLaunchKernelGGL((fit6<true, true>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    default: hipLaunchKernelGGL((fit6<false, true>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
