@@ -40,7 +40,11 @@ CONFIGS = {
            "ptm6-relight 3840x2160, 1000 random (lu,lv) streamed one per launch, fp32 out (BASELINE configs[4])"),
     "c6": ("perpixel", 2160, 3840, 100, 1, "ptm",
            "ptm6 per-pixel fit 3840x2160 N=100, light vectors from camera positions in-kernel (reference geometry)"),
+    "c7": ("operator", 400, 400, 100, 1, "rbf",
+           "linear-RBF interpolation (reference default, SciPy Rbf) of a 400x400 ROI x 100 shared lights on the "
+           "100x100 grid -> int32 tables (interpolate_intensities + prepare_images_data)"),
 }
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
 
 
 def synth_dirs(n, seed, radius=0.9):
@@ -281,7 +285,67 @@ class PerPixelWorkload:
                           f"{self.N} lights, {reps} reps in {el:.1f}s; {name}"}
 
 
-WORKLOADS = {"fit": FitWorkload, "relight": RelightWorkload, "perpixel": PerPixelWorkload}
+class OperatorWorkload:
+    """One step = one rti_apply_operator launch: RBF operator (E = 100x100 grid) over the ROI stack -> int32."""
+
+    def __init__(self, args, cfg, rank, dev):
+        import rti
+
+        self.rti = rti
+        _, H, W, N, C, basis, desc = cfg
+        self.H, self.W, self.N, self.desc = H, W, N, desc
+        self.P = P = H * W
+        self.lu, self.lv = synth_dirs(N, seed=2)
+        self.I = synth_stack(H, W, N, 1, "ptm", self.lu, self.lv, seed=1000 + rank, device=dev)[0]  # [N, P]
+        xf = np.around(np.mgrid[-1:1:0.02, -1:1:0.02][1], 2)[0]
+        self.qu, self.qv = np.tile(xf, xf.size), np.repeat(xf, xf.size)
+        self.E = E = self.qu.size
+        self.op64 = rti.rbf_operator(self.lu, self.lv, self.qu, self.qv)  # [N, E] fp64 (host, one-time)
+        self.op = torch.as_tensor(self.op64.astype(np.float32), device=dev).contiguous()
+        self.out = torch.empty((E, P), dtype=torch.int32, device=dev)
+        self.units = P * E
+        self.alg_bytes = 4.0 * P * N + 4.0 * P * E  # stack read once + int32 tables written
+        self.flops = 2.0 * E * N * P
+        self.metric = f"Mpix*evals/sec {desc}"
+        self.unit = "Mpix*evals/s"
+        import ctypes
+
+        self.ctypes = ctypes
+        self.lib = rti._lib.lib()
+
+    def step(self, i):
+        c = self.ctypes
+        L = self.rti._lib
+        st = self.lib.rti_apply_operator(c.c_void_p(self.op.data_ptr()), self.E, self.N, self.E,
+                                         c.c_void_p(self.I.data_ptr()), L.RTI_F32, self.P, 1, self.P, self.N * self.P,
+                                         c.c_void_p(self.out.data_ptr()), L.RTI_I32, self.P, self.E * self.P,
+                                         c.c_void_p(torch.cuda.current_stream().cuda_stream))
+        L.check(st, "rti_apply_operator")
+
+    def config(self):
+        return {"lights": self.N, "evals": self.E, "basis": "rbf-linear", "out": "int32 tables [E][P]"}
+
+    def roofline(self, kernel_ms):
+        ach = self.flops / (kernel_ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None, "kernel_ms": round(kernel_ms, 4),
+                "alg_flops_per_launch": self.flops, "alg_bytes_per_launch": self.alg_bytes,
+                "hbm_GBps": round(self.alg_bytes / (kernel_ms * 1e-3) / 1e9, 1)}
+
+    def cpu_baseline(self, budget_s):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        npx = 256
+        I = self.I[:, :npx].cpu().numpy().astype(np.float64)
+        op = self.op64
+        rate, reps, el = cpu_sample_rate(lambda: (op.T @ I).astype(np.int32), npx * self.E, budget_s)
+        threads, name = cpu_info()
+        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"NumPy fp64 operator product (the SciPy-Rbf-equivalent grid) on {npx} px x {self.E} "
+                          f"evals, {reps} reps in {el:.1f}s; {name}"}
+
+
+WORKLOADS = {"fit": FitWorkload, "relight": RelightWorkload, "perpixel": PerPixelWorkload,
+             "operator": OperatorWorkload}
 
 
 def main():
@@ -302,7 +366,7 @@ def main():
     cfg = CONFIGS[args.config]
     kind = cfg[0]
     if args.steps is None:
-        args.steps = {"fit": 20, "relight": 1000, "perpixel": 10}[kind]
+        args.steps = {"fit": 20, "relight": 1000, "perpixel": 10, "operator": 10}[kind]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -390,12 +454,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32" if kind != "perpixel" else "f32 in / f64 solve",
+            "dtype": {"perpixel": "f32 in / f64 solve", "operator": "f32 (MFMA) -> int32"}.get(kind, "f32"),
             "data": "synthetic (seeded smooth PTM/HSH coefficient fields + N(0,2) noise, rounded to 0..255, fp32)",
             "config": conf,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(workload_key),
-                         "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": wl.alg_bytes},
+            "roofline": wl.roofline(kernel_ms) if hasattr(wl, "roofline") else {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(workload_key),
+                "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": wl.alg_bytes},
             "cpu_baseline": cpu,
         }
         if gather_ms is not None:

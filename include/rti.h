@@ -37,6 +37,7 @@ extern "C" {
 #define RTI_ERR_BAD_ARG     1   /* null pointer, non-positive size, k/N mismatch, N < k */
 #define RTI_ERR_UNSUPPORTED 2   /* valid but unsupported combination (dtype/basis/layout) */
 #define RTI_ERR_HIP         3   /* HIP runtime error at launch */
+#define RTI_ERR_SINGULAR    4   /* singular system (the reference's SciPy Rbf raises LinAlgError) */
 
 /* ---- bases ---- */
 #define RTI_BASIS_PTM6  0   /* (lu², lv², lu·lv, lu, lv, 1), analysis.py:285 */
@@ -128,6 +129,35 @@ int rti_fit_perpixel_cam(const double* cams, int N,
 int rti_fit_perpixel_dirs(const float* lu, const float* lv, const void* I, int in_dtype,
                           int N, int64_t P, double rcond,
                           void* coef, int coef_dtype, int coef_layout, rti_stream_t stream);
+
+/* ---- host: light operators for a SHARED light set ---------------------------------
+ * A light operator maps the N intensities of a pixel to E outputs: out_e = Σ_n M[e][n] I_n.
+ * Both builders return it LIGHT-MAJOR, opT[n][e] (row stride E), fp64, ready for
+ * rti_apply_operator after a cast to fp32.
+ * rti_rbf_operator: the reference's default interpolator, SciPy Rbf(lu, lv, I,
+ *   function='linear') evaluated at (qu_e, qv_e) (analysis.py:249-260):
+ *   A_ij = ‖x_i − x_j‖, Φ_ej = ‖q_e − x_j‖, M = Φ A⁻¹ (LU with partial pivoting, fp64).
+ *   Returns RTI_ERR_SINGULAR for a singular A (e.g. duplicate light directions), where
+ *   SciPy raises LinAlgError.
+ * rti_basis_operator: M = B(q) · pinv for PTM/HSH — the fit and the grid evaluation
+ *   (analysis.py:293-315) fused into one operator (rcond as in rti_pinv). */
+int rti_rbf_operator(const float* lu, const float* lv, int n, const double* qu, const double* qv, int E,
+                     double* opT);
+int rti_basis_operator(int basis, const float* lu, const float* lv, int n, const double* qu, const double* qv,
+                       int E, double rcond, double* opT);
+
+/* ---- device: apply a light operator (MFMA) -------------------------------------------
+ * out[c][e][p] = Σ_n opT[n][e] · I[c][n][p]   (v_mfma_f32_16x16x4_f32, fp32 accumulate)
+ * opT: device fp32 [N][op_stride] (op_stride >= E).  I as in rti_fit_shared.
+ * out: device, out_dtype F32 / F64 / I32 (C truncation, NaN → INT32_MIN) / U8 (clipped),
+ * element (c, e, p) at c*out_channel_stride + e*out_row_stride + p (0 = dense).
+ * With the RBF operator on the 100×100 grid this is interpolate_intensities +
+ * prepare_images_data for the reference's default method in one pass. */
+int rti_apply_operator(const float* opT, int E, int N, int64_t op_stride,
+                       const void* I, int in_dtype, int64_t P, int C,
+                       int64_t light_stride, int64_t channel_stride,
+                       void* out, int out_dtype, int64_t out_row_stride, int64_t out_channel_stride,
+                       rti_stream_t stream);
 
 /* ---- device: light vectors ---------------------------------------------------------
  * The light-vector half of compute_intensities (analysis.py:221-231) for an

@@ -124,6 +124,54 @@ static void jacobi_pinv(const double* A, int n, int k, double rcond, double* pin
     }
 }
 
+// LU factorisation with partial pivoting (LAPACK getrf semantics), in place, row-major n×n.
+// Returns false for an exactly singular matrix (a zero pivot), as dgesv reports info > 0.
+static bool lu_factor(std::vector<double>& a, int n, std::vector<int>& piv) {
+  piv.resize(n);
+  for (int k = 0; k < n; ++k) {
+    int p = k;
+    double best = std::fabs(a[(size_t)k * n + k]);
+    for (int i = k + 1; i < n; ++i) {
+      const double v = std::fabs(a[(size_t)i * n + k]);
+      if (v > best) best = v, p = i;
+    }
+    piv[k] = p;
+    if (best == 0.0) return false;
+    if (p != k)
+      for (int j = 0; j < n; ++j) std::swap(a[(size_t)k * n + j], a[(size_t)p * n + j]);
+    const double inv = 1.0 / a[(size_t)k * n + k];
+    for (int i = k + 1; i < n; ++i) {
+      double& l = a[(size_t)i * n + k];
+      l *= inv;
+      if (l == 0.0) continue;
+      for (int j = k + 1; j < n; ++j) a[(size_t)i * n + j] -= l * a[(size_t)k * n + j];
+    }
+  }
+  return true;
+}
+
+// Solve A X = B for X, B row-major n×m (overwritten), with the factors of lu_factor.
+static void lu_solve(const std::vector<double>& a, const std::vector<int>& piv, int n, double* B, int m) {
+  for (int k = 0; k < n; ++k)
+    if (piv[k] != k)
+      for (int j = 0; j < m; ++j) std::swap(B[(size_t)k * m + j], B[(size_t)piv[k] * m + j]);
+  for (int i = 1; i < n; ++i)
+    for (int k = 0; k < i; ++k) {
+      const double l = a[(size_t)i * n + k];
+      if (l == 0.0) continue;
+      for (int j = 0; j < m; ++j) B[(size_t)i * m + j] -= l * B[(size_t)k * m + j];
+    }
+  for (int i = n - 1; i >= 0; --i) {
+    for (int k = i + 1; k < n; ++k) {
+      const double u = a[(size_t)i * n + k];
+      if (u == 0.0) continue;
+      for (int j = 0; j < m; ++j) B[(size_t)i * m + j] -= u * B[(size_t)k * m + j];
+    }
+    const double inv = 1.0 / a[(size_t)i * n + i];
+    for (int j = 0; j < m; ++j) B[(size_t)i * m + j] *= inv;
+  }
+}
+
 }  // namespace rti
 
 using namespace rti;
@@ -138,6 +186,7 @@ const char* rti_status_string(int status) {
     case RTI_ERR_BAD_ARG: return "bad argument";
     case RTI_ERR_UNSUPPORTED: return "unsupported";
     case RTI_ERR_HIP: return "hip error";
+    case RTI_ERR_SINGULAR: return "singular matrix";
     default: return "unknown status";
   }
 }
@@ -169,6 +218,52 @@ int rti_pinv(int basis, const float* lu, const float* lv, int n, double rcond, d
   std::vector<double> A((size_t)n * k);
   for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], A.data() + (size_t)i * k);
   jacobi_pinv(A.data(), n, k, rcond, pinv);
+  return RTI_OK;
+}
+
+int rti_rbf_operator(const float* lu, const float* lv, int n, const double* qu, const double* qv, int E,
+                     double* opT) {
+  if (!lu || !lv || !qu || !qv || !opT || n <= 0 || E <= 0)
+    return fail(RTI_ERR_BAD_ARG, "rti_rbf_operator: null pointer or non-positive size");
+  // nodes as SciPy holds them: float64 copies of the float32 light vectors
+  std::vector<double> x(n), y(n);
+  for (int i = 0; i < n; ++i) x[i] = (double)lu[i], y[i] = (double)lv[i];
+  std::vector<double> A((size_t)n * n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      const double dx = x[i] - x[j], dy = y[i] - y[j];
+      A[(size_t)i * n + j] = std::sqrt(dx * dx + dy * dy);  // pdist 'euclidean', linear kernel r
+    }
+  std::vector<int> piv;
+  if (!lu_factor(A, n, piv)) return fail(RTI_ERR_SINGULAR, "rti_rbf_operator: Matrix is singular.");
+  // X = A^-1 Φᵀ (n×E): A is symmetric, so row n of X is column n of M = Φ A^-1, i.e. opT[n][e]
+  for (int j = 0; j < n; ++j)
+    for (int e = 0; e < E; ++e) {
+      const double dx = qu[e] - x[j], dy = qv[e] - y[j];
+      opT[(size_t)j * E + e] = std::sqrt(dx * dx + dy * dy);
+    }
+  lu_solve(A, piv, n, opT, E);
+  return RTI_OK;
+}
+
+int rti_basis_operator(int basis, const float* lu, const float* lv, int n, const double* qu, const double* qv,
+                       int E, double rcond, double* opT) {
+  const int k = basis_terms(basis);
+  if (k < 0) return fail(RTI_ERR_BAD_ARG, "rti_basis_operator: unknown basis %d", basis);
+  if (!lu || !lv || !qu || !qv || !opT || n <= 0 || E <= 0)
+    return fail(RTI_ERR_BAD_ARG, "rti_basis_operator: null pointer or non-positive size");
+  if (n < k) return fail(RTI_ERR_BAD_ARG, "rti_basis_operator: %d lights < %d basis terms", n, k);
+  std::vector<double> A((size_t)n * k), pinv((size_t)k * n), b(k);
+  for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], A.data() + (size_t)i * k);
+  jacobi_pinv(A.data(), n, k, rcond, pinv.data());
+  for (int e = 0; e < E; ++e) {
+    basis_eval<double>(basis, qu[e], qv[e], b.data());
+    for (int j = 0; j < n; ++j) {
+      double s = 0.0;
+      for (int i = 0; i < k; ++i) s += b[i] * pinv[(size_t)i * n + j];
+      opT[(size_t)j * E + e] = s;
+    }
+  }
   return RTI_OK;
 }
 

@@ -24,30 +24,13 @@
 #include <type_traits>
 
 #include "rti_basis.h"
+#include "rti_convert.h"
 #include "rti_internal.h"
 
 namespace rti {
 namespace {
 
 constexpr int ECH = 64;  // evals per eval-major block (basis table in LDS)
-
-template <typename TC>
-__device__ __forceinline__ int32_t trunc_i32(TC v) {
-  // C truncation toward zero; NaN / out of range -> INT32_MIN (x86 cvttsd2si,
-  // which is what NumPy's float64 -> int32 element assignment produces).
-  return (v >= TC(-2147483648.0) && v < TC(2147483648.0)) ? (int32_t)v : INT32_MIN;
-}
-
-template <typename TO, typename TC>
-__device__ __forceinline__ TO cvt_out(TC v) {
-  if constexpr (std::is_same<TO, float>::value) return (float)v;
-  else if constexpr (std::is_same<TO, double>::value) return (double)v;
-  else if constexpr (std::is_same<TO, int32_t>::value) return trunc_i32(v);
-  else {
-    const int32_t i = trunc_i32(v);
-    return (uint8_t)(i > 255 ? 255 : (i <= 0 ? 0 : i));
-  }
-}
 
 // fp64: the reference's order, every product and sum rounded (analysis.py:307-312).
 template <int K>

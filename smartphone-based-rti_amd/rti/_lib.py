@@ -18,6 +18,7 @@ RTI_OK = 0
 RTI_ERR_BAD_ARG = 1
 RTI_ERR_UNSUPPORTED = 2
 RTI_ERR_HIP = 3
+RTI_ERR_SINGULAR = 4
 
 RTI_BASIS_PTM6 = 0
 RTI_BASIS_HSH16 = 1
@@ -78,6 +79,11 @@ SIGNATURES = {
                                        _c_void_p, _c_int, _c_int, _c_void_p]),
     "rti_light_dirs": (_c_int, [_c_void_p, _c_int, _c_int, _c_int, _c_double, _c_double, _c_void_p, _c_void_p,
                                 _c_void_p]),
+    "rti_rbf_operator": (_c_int, [_c_float_p, _c_float_p, _c_int, _c_double_p, _c_double_p, _c_int, _c_double_p]),
+    "rti_basis_operator": (_c_int, [_c_int, _c_float_p, _c_float_p, _c_int, _c_double_p, _c_double_p, _c_int, _c_double,
+                                    _c_double_p]),
+    "rti_apply_operator": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_void_p, _c_int, _c_i64, _c_int, _c_i64,
+                                    _c_i64, _c_void_p, _c_int, _c_i64, _c_i64, _c_void_p]),
     "rti_relight": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_int, _c_void_p, _c_int, _c_void_p, _c_int,
                              _c_int, _c_void_p]),
 }
@@ -115,4 +121,8 @@ def check(status, fn_name):
         raise ValueError(msg)
     if status == RTI_ERR_UNSUPPORTED:
         raise NotImplementedError(msg)
+    if status == RTI_ERR_SINGULAR:
+        import numpy as np
+
+        raise np.linalg.LinAlgError(msg)  # what the reference's SciPy Rbf raises
     raise RTIError(status, msg)

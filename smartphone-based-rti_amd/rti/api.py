@@ -280,3 +280,76 @@ def relight(coef, lu, lv, basis="ptm", *, layout="pixel", out_dtype=torch.float3
     if scalar:
         return out[0] if ol == L.RTI_OUT_EVAL_MAJOR else out[..., 0]
     return out
+
+
+# ---- light operators (RBF, fused PTM/HSH fit + evaluation) ----------------------------------
+
+def _query(qu, qv):
+    qu = np.ascontiguousarray(np.asarray(qu, np.float64).ravel())
+    qv = np.ascontiguousarray(np.asarray(qv, np.float64).ravel())
+    if qu.size != qv.size or qu.size == 0:
+        raise ValueError("query directions: qu and qv must be non-empty and of equal length")
+    return qu, qv
+
+
+def rbf_operator(lu, lv, qu, qv):
+    """Host fp64 linear-RBF operator opT[N, E] (SciPy Rbf 'linear', analysis.py:249-260).
+
+    Raises numpy.linalg.LinAlgError for a singular system, as SciPy does."""
+    lu, lv = _f32_host(lu, "lu"), _f32_host(lv, "lv")
+    if lu.size != lv.size:
+        raise ValueError("lu and lv differ in length")
+    qu, qv = _query(qu, qv)
+    out = np.empty((lu.size, qu.size), np.float64)
+    L.check(L.lib().rti_rbf_operator(_fptr(lu), _fptr(lv), lu.size, _dptr(qu), _dptr(qv), qu.size, _dptr(out)),
+            "rti_rbf_operator")
+    return out
+
+
+def basis_operator(lu, lv, qu, qv, basis="ptm", rcond=None):
+    """Host fp64 operator opT[N, E] = (B(q) · pinv)ᵀ: fit and evaluation fused (analysis.py:293-315)."""
+    lu, lv = _f32_host(lu, "lu"), _f32_host(lv, "lv")
+    if lu.size != lv.size:
+        raise ValueError("lu and lv differ in length")
+    qu, qv = _query(qu, qv)
+    out = np.empty((lu.size, qu.size), np.float64)
+    rc = -1.0 if rcond is None else float(rcond)
+    L.check(L.lib().rti_basis_operator(basis_id(basis), _fptr(lu), _fptr(lv), lu.size, _dptr(qu), _dptr(qv),
+                                       qu.size, rc, _dptr(out)), "rti_basis_operator")
+    return out
+
+
+def apply_operator(opT, I, out_dtype=torch.float32):
+    """out[.., E, H, W] = Σ_n opT[n, e] · I[.., n, H, W] on the GPU (MFMA).
+
+    opT: [N, E] operator (host array or CUDA tensor; cast to fp32).  I: CUDA
+    [N, H, W], [N, P] or [C, N, H, W], fp32/u8/int32, light-major."""
+    _require_cuda(I, "I")
+    odt = _OUT_DTYPES.get(out_dtype)
+    if odt is None:
+        raise ValueError("out_dtype must be float32, float64, int32 or uint8")
+    op = torch.as_tensor(opT, device=I.device).to(torch.float32).contiguous()
+    N, E = op.shape
+    if I.dim() == 2:
+        C, spatial = 1, (I.shape[1],)
+    elif I.dim() == 3:
+        C, spatial = 1, tuple(I.shape[1:])
+    elif I.dim() == 4:
+        C, spatial = I.shape[0], tuple(I.shape[2:])
+    else:
+        raise ValueError("I must be [N, P], [N, H, W] or [C, N, H, W]")
+    n_img = I.shape[-3] if I.dim() >= 3 else I.shape[0]
+    if n_img != N:
+        raise ValueError(f"operator has {N} lights, I has {n_img}")
+    P = int(np.prod(spatial))
+    Ic = I.contiguous()
+    out = torch.empty((C, E) + spatial, dtype=out_dtype, device=I.device)
+    st = L.lib().rti_apply_operator(_vp(op), E, N, E, _vp(Ic), _IN_DTYPES[Ic.dtype], P, C, P, N * P, _vp(out), odt, P,
+                                    E * P, _stream_of(I))
+    L.check(st, "rti_apply_operator")
+    return out if I.dim() == 4 else out[0]
+
+
+def interpolate_rbf(I, lu, lv, qu, qv, out_dtype=torch.float32):
+    """Linear-RBF interpolation of every pixel at (qu, qv) for a SHARED light set -> [.., E, H, W]."""
+    return apply_operator(rbf_operator(lu, lv, qu, qv), I, out_dtype=out_dtype)

@@ -8,7 +8,9 @@ reference                       file:line                                    HIP
 ==============================  ===========================================  ==============================
 compute_intensities             analysis.py:196-246                          rti_light_dirs
 _interpolate_PTM                analysis.py:263-317                          rti_fit_perpixel_dirs (P=1) + rti_relight
+_interpolate_RBF                analysis.py:249-260                          rti_rbf_operator + rti_apply_operator
 interpolate_intensities (PTM)   analysis.py:321-372                          rti_fit_perpixel_dirs + rti_relight (pixel-major)
+interpolate_intensities (RBF)   analysis.py:321-372 (default method)         rti_rbf_operator + rti_apply_operator
 prepare_images_data             analysis.py:375-411                          layout adapter (torch); native: relight_tables
 relighting_event lookup         interactive_relighting.py:11-39              table lookup + clip (host, one image)
 ==============================  ===========================================  ==============================
@@ -18,8 +20,10 @@ arrays with the reference's dtypes.  The reference returns nested lists; here
 the same indexing ([y][x][ly][lx], [ly][lx][y][x]) works on ndarrays.
 Differences, by design:
   * the ROI size is the data's size, not ``constants.ROI_DIAMETER``;
-  * the RBF branch (``interpolate_PTM=False``, the reference's default) is the
-    next row of SURVEY §8(f) and raises ``NotImplementedError`` for now;
+  * the RBF branch (``interpolate_PTM=False``, the reference's default) runs
+    when every pixel sees the same light directions (directional lights: one
+    shared operator); per-pixel light lists with RBF raise ``NotImplementedError``
+    for now;
   * the debug plots of ``first_only=True`` are not drawn (first pixel only is kept).
 """
 from __future__ import annotations
@@ -92,15 +96,35 @@ def _interpolate_PTM(x_coarse, y_coarse, xy_fine, intensity_values, device=None)
     return out.reshape(G, G).cpu().numpy()
 
 
+def _interpolate_RBF(x_coarse, y_coarse, x_fine, y_fine, intensity_values, device=None):
+    """analysis.py:249-260: SciPy Rbf(x, y, I, function='linear')(x_fine, y_fine) for one pixel, f64.
+
+    A singular node set (e.g. repeated directions) raises numpy.linalg.LinAlgError like SciPy."""
+    dev = _device(device)
+    xf = np.asarray(x_fine, np.float64)
+    op = api.rbf_operator(x_coarse, y_coarse, xf.ravel(), np.asarray(y_fine, np.float64).ravel())
+    it = np.asarray(intensity_values)
+    if it.dtype not in (np.float32, np.int32, np.uint8):
+        it = it.astype(np.int32)
+    I = torch.as_tensor(np.ascontiguousarray(it.reshape(-1, 1)), device=dev)
+    out = api.apply_operator(op, I, out_dtype=torch.float64)
+    return out.reshape(xf.shape).cpu().numpy()
+
+
+def _shared_directions(lx, ly):
+    """True when every pixel holds the same light list (directional lights)."""
+    return bool((lx == lx[:1, :1]).all() and (ly == ly[:1, :1]).all())
+
+
 def interpolate_intensities(data, interpolate_PTM=False, first_only=False, device=None):
     """analysis.py:321-372 -> ndarray [R, R, G, G] f64 indexed [y][x][ly][lx]."""
     if data is None or len(data) != 3:
         raise Exception("Error computing interpolation: results are empty or invalid")
-    if not interpolate_PTM:
-        raise NotImplementedError("linear RBF interpolation (analysis.py:249-260) is the next row (SURVEY §8(f)-1)")
     lx, ly, inten = (np.asarray(d) for d in data)
     R = 1 if first_only else lx.shape[0]
     lx, ly, inten = lx[:R, :R], ly[:R, :R], inten[:R, :R]
+    if not interpolate_PTM:
+        return _interpolate_rbf_roi(lx, ly, inten, device)
     if lx.shape[-1] < 6:
         raise ValueError(f"shapes not aligned: {lx.shape[-1]} lights < 6 PTM terms")
     dev = _device(device)
@@ -108,6 +132,29 @@ def interpolate_intensities(data, interpolate_PTM=False, first_only=False, devic
     G, lu, lv = _grid_luv(grid_axis())
     out = api.relight(coef, lu, lv, basis="ptm", out_dtype=torch.float64, out_layout="pixel")
     return out.reshape(R, R, G, G).cpu().numpy()
+
+
+def _interpolate_rbf_roi(lx, ly, inten, device):
+    """RBF branch of interpolate_intensities (analysis.py:360-363) for a shared light list."""
+    if not _shared_directions(lx, ly):
+        raise NotImplementedError("linear RBF with per-pixel light directions is not implemented yet; "
+                                  "directional (shared) light lists run on the GPU operator path")
+    dev = _device(device)
+    R, N = lx.shape[0], lx.shape[-1]
+    G, qu, qv = _grid_luv(grid_axis())
+    op = api.rbf_operator(lx[0, 0], ly[0, 0], qu, qv)
+    it = inten if inten.dtype in (np.float32, np.int32, np.uint8) else inten.astype(np.int32)
+    I = torch.as_tensor(np.ascontiguousarray(it.reshape(R * R, N).T), device=dev)  # light-major [N, P]
+    out = api.apply_operator(op, I, out_dtype=torch.float64)  # [E, P]
+    return out.T.reshape(R, R, G, G).cpu().numpy()
+
+
+def rbf_tables(I, lu, lv, step=INTERPOLATION_PARAM):
+    """Native fused RBF path: light-major stack [N, H, W] -> int32 tables [G, G, H, W]
+    (interpolate_intensities(RBF) + prepare_images_data in one operator launch)."""
+    G, qu, qv = _grid_luv(grid_axis(step))
+    out = api.apply_operator(api.rbf_operator(lu, lv, qu, qv), I, out_dtype=torch.int32)
+    return out.reshape((G, G) + tuple(out.shape[1:]))
 
 
 def prepare_images_data(data, first_only=False, device=None):

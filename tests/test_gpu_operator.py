@@ -1,0 +1,106 @@
+"""GPU parity of the light-operator path (rti_apply_operator): the reference's
+default linear-RBF interpolation (SciPy Rbf goldens) and the fused PTM/HSH
+fit + grid evaluation, against the oracle."""
+import numpy as np
+import pytest
+import torch
+
+import rti
+import rti_oracle as o
+from conftest import golden, relight_close
+from rti import compat
+
+pytestmark = pytest.mark.gpu
+
+
+def grid_q():
+    xf = o.grid_axis()
+    return np.tile(xf, 100), np.repeat(xf, 100)
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("in_dtype", [torch.int32, torch.float32, torch.uint8])
+def test_rbf_grid_matches_scipy_golden(cuda, out_dtype, in_dtype):
+    d = golden("rbf_shared_4px_N20.npz")
+    qu, qv = grid_q()
+    I = torch.as_tensor(np.ascontiguousarray(d["I"].T)).to(cuda).to(in_dtype)  # [N, 4 px]
+    out = rti.interpolate_rbf(I, d["lu"], d["lv"], qu, qv, out_dtype=out_dtype).cpu().numpy()
+    got = out.T.reshape(-1, 100, 100)
+    err, ok = relight_close(got, d["grid"])
+    assert ok, err
+
+
+def test_compat_interpolate_rbf_single_pixel(cuda):
+    d = golden("rbf_shared_4px_N20.npz")
+    yi, xi = np.mgrid[-1:1:0.02, -1:1:0.02]
+    xi, yi = np.around(xi, 2), np.around(yi, 2)
+    for p in range(4):
+        g = compat._interpolate_RBF(d["lu"], d["lv"], xi, yi, d["I"][p])
+        assert g.shape == (100, 100) and g.dtype == np.float64
+        err, ok = relight_close(g, d["grid"][p])
+        assert ok, err
+
+
+def test_compat_interpolate_intensities_default_rbf(cuda):
+    d = golden("rbf_shared_4px_N20.npz")
+    N = len(d["lu"])
+    lx = np.broadcast_to(d["lu"], (2, 2, N)).copy()
+    ly = np.broadcast_to(d["lv"], (2, 2, N)).copy()
+    inten = d["I"].reshape(2, 2, N)
+    grid = compat.interpolate_intensities((lx, ly, inten))  # default = RBF (analysis.py:321)
+    assert grid.shape == (2, 2, 100, 100)
+    err, ok = relight_close(grid.reshape(4, 100, 100), d["grid"])
+    assert ok, err
+    tables = compat.prepare_images_data(grid)
+    ref_t = np.transpose(d["grid"].reshape(2, 2, 100, 100), (2, 3, 0, 1)).astype(np.int32)
+    near = np.abs(np.transpose(d["grid"].reshape(2, 2, 100, 100), (2, 3, 0, 1)) % 1.0)
+    near = np.minimum(near, 1 - near) < 1e-3
+    assert not ((tables != ref_t) & ~near).any()
+    fused = compat.rbf_tables(torch.as_tensor(np.ascontiguousarray(d["I"].T.reshape(N, 2, 2)), device=cuda),
+                              d["lu"], d["lv"]).cpu().numpy()
+    assert not ((fused != ref_t) & ~near).any()
+    lx2 = lx.copy()
+    lx2[1, 1, 0] += 0.01
+    with pytest.raises(NotImplementedError):
+        compat.interpolate_intensities((lx2, ly, inten))
+
+
+def test_rbf_singular_raises_linalgerror(cuda):
+    lu = np.array([0.1, 0.1, 0.5, -0.2], np.float32)
+    lv = np.array([0.2, 0.2, 0.0, 0.3], np.float32)
+    with pytest.raises(np.linalg.LinAlgError):
+        rti.rbf_operator(lu, lv, [0.0], [0.0])
+
+
+@pytest.mark.parametrize("hw,n,E", [((1, 1), 6, 1), ((3, 5), 7, 3), ((17, 33), 13, 100), ((64, 65), 37, 257),
+                                    ((31, 128), 50, 1000), ((8, 8), 256, 70)])
+def test_operator_ragged_vs_oracle(cuda, hw, n, E):
+    h, w = hw
+    lu, lv = o.synth_dirs(n, n)
+    I = o.synth_intensities(h, w, lu, lv, seed=h + w)
+    rng = np.random.default_rng(E)
+    qu, qv = rng.uniform(-1, 1, E), rng.uniform(-1, 1, E)
+    op = rti.basis_operator(lu, lv, qu, qv, "ptm")  # fused fit + evaluation
+    out = rti.apply_operator(op, torch.as_tensor(I, device=cuda)).cpu().numpy()
+    coef = o.fit_shared(I, o.pinv_shared("ptm", lu, lv))
+    ref = o.relight(coef, "ptm", qu, qv).reshape(E, h, w)
+    err, ok = relight_close(out, ref, rtol=1e-5)
+    assert ok, err
+
+
+def test_operator_channels_and_int_outputs(cuda):
+    lu, lv = o.synth_dirs(30, 2)
+    planes = np.stack([o.synth_intensities(20, 24, lu, lv, seed=s) for s in (1, 2, 3)])  # [3, N, H, W]
+    qu, qv = grid_q()
+    op = rti.rbf_operator(lu, lv, qu[:500], qv[:500])
+    I = torch.as_tensor(planes, device=cuda)
+    f = rti.apply_operator(op, I, out_dtype=torch.float64).cpu().numpy()
+    assert f.shape == (3, 500, 20, 24)
+    ref = np.einsum("ne,cnhw->cehw", op, planes.astype(np.float64))
+    err, ok = relight_close(f, ref)
+    assert ok, err
+    i32 = rti.apply_operator(op, I, out_dtype=torch.int32).cpu().numpy()
+    u8 = rti.apply_operator(op, I, out_dtype=torch.uint8).cpu().numpy()
+    frac = np.abs(ref - np.round(ref)) > 1e-3
+    assert np.array_equal(i32[frac], np.trunc(ref[frac]).astype(np.int32))
+    assert np.array_equal(u8[frac], np.clip(np.trunc(ref[frac]), 0, 255).astype(np.uint8))

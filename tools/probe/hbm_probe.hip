@@ -101,10 +101,15 @@ __global__ void __launch_bounds__(256) fit6(const float* __restrict__ pinv, cons
 //   0 plain float4 pixel-major   1 sc1 (write-through, drop from L2) buffer stores   2 sc0|sc1
 //   3 nt buffer stores           4 all waves store into one 64 KiB window (L2-resident)
 //   5 planar float4 (1 KiB contiguous per wave instruction)   6 dword stores pixel-major
-template <int SM>
+template <int SM, bool XCD = false>
 __global__ void __launch_bounds__(256) fit6_store(const float* __restrict__ pinv, const float* __restrict__ I, int N,
-                                                  int64_t P, float* __restrict__ coef) {
-  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+                                                  int64_t P, float* __restrict__ coef, int64_t wmask = 16383) {
+  int64_t bid = blockIdx.x;
+  if constexpr (XCD) {  // blocks b, b+8, ... share an XCD: give each XCD one contiguous eighth of the image
+    const int64_t nb = gridDim.x, per = nb / 8;
+    if (bid < per * 8) bid = (bid % 8) * per + bid / 8;
+  }
+  const int64_t p0 = (bid * 256 + threadIdx.x) * 4;
   if (p0 >= P) return;
   float acc[6][4] = {};
   const float* src = I + p0;
@@ -142,7 +147,7 @@ __global__ void __launch_bounds__(256) fit6_store(const float* __restrict__ pinv
 #pragma unroll
     for (int i = 0; i < 24; ++i) coef[p0 * 6 + i] = o[i];
   } else if constexpr (SM == 0 || SM == 4) {
-    float* d = SM == 0 ? coef + p0 * 6 : coef + ((p0 * 6) & 16383);
+    float* d = SM == 0 ? coef + p0 * 6 : coef + ((p0 * 6) & wmask);
 #pragma unroll
     for (int i = 0; i < 24; i += 4) *reinterpret_cast<floatx4*>(d + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
   } else {
@@ -168,7 +173,13 @@ extern "C" int probe_store(const float* pinv, const float* I, int N, int64_t P, 
     case 3: hipLaunchKernelGGL((fit6_store<3>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
     case 4: hipLaunchKernelGGL((fit6_store<4>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
     case 5: hipLaunchKernelGGL((fit6_store<5>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
-    default: hipLaunchKernelGGL((fit6_store<6>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 6: hipLaunchKernelGGL((fit6_store<6>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 7: hipLaunchKernelGGL((fit6_store<0, true>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    case 8: hipLaunchKernelGGL((fit6_store<5, true>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
+    default: {  // variant >= 100: stores wrap inside a window of (variant - 100) MiB
+      const int64_t floats = (int64_t)(variant - 100) * 262144;
+      hipLaunchKernelGGL((fit6_store<4>), grid, dim3(256), 0, s, pinv, I, N, P, coef, floats - 1);
+    }
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
@@ -196,5 +207,16 @@ extern "C" int probe_fit6(const float* pinv, const float* I, int N, int64_t P, f
     case 2: hipLaunchKernelGGL((fit6<true, true>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
     default: hipLaunchKernelGGL((fit6<false, true>), grid, dim3(256), 0, s, pinv, I, N, P, coef); break;
   }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// Pure write of `bytes` (16 B per lane, contiguous), for the phase-separated lower bound.
+__global__ void __launch_bounds__(256) write_stream(float* __restrict__ out, int64_t n4) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) reinterpret_cast<floatx4*>(out)[i] = floatx4{1.f, 2.f, 3.f, (float)i};
+}
+extern "C" int probe_write(float* out, int64_t bytes, void* stream) {
+  const int64_t n4 = bytes / 16;
+  hipLaunchKernelGGL(write_stream, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out, n4);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

@@ -61,11 +61,12 @@ def main():
         for pvnt in (0, 1, 2, 3, 4):
             variants.append((f"probe_read_v{pvnt}", "probe", str(pvnt), 0))
         probe.probe_store.argtypes = probe.probe_fit6.argtypes
+        probe.probe_write.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+        variants.append(("probe_write_coef_bytes", "pwrite", "0", 0))
         if k == 6:
             for pvnt, nm in ((1, "nostore"),):
                 variants.append((f"probe_fit6_{nm}", "pfit", str(pvnt), 0))
-            for pvnt, nm in ((0, "plain"), (1, "sc1"), (2, "sc0sc1"), (3, "nt"), (4, "l2window"), (5, "planar"),
-                             (6, "dword")):
+            for pvnt, nm in ((0, "plain"), (5, "planar"), (7, "plain_xcd"), (8, "planar_xcd"), (4, "win64K")):
                 variants.append((f"probe_store_{nm}", "pstore", str(pvnt), 0))
     stream = torch.cuda.current_stream(dev)
     times = {name: [] for name, *_ in variants}
@@ -74,8 +75,10 @@ def main():
         if kern == "probe":
             probe.probe_read(ctypes.c_void_p(I.data_ptr()), N, P, ctypes.c_void_p(sink.data_ptr()), int(layout),
                              ctypes.c_void_p(stream.cuda_stream))
+        elif kern == "pwrite":
+            probe.probe_write(ctypes.c_void_p(coefs["pixel"].data_ptr()), 4 * P * k, ctypes.c_void_p(stream.cuda_stream))
         elif kern == "pstore":
-            tgt = coefs["planar"] if layout == "5" else coefs["pixel"]
+            tgt = coefs["planar"] if layout in ("5", "8") else coefs["pixel"]
             probe.probe_store(ctypes.c_void_p(pv.data_ptr()), ctypes.c_void_p(I.data_ptr()), N, P,
                               ctypes.c_void_p(tgt.data_ptr()), int(layout), ctypes.c_void_p(stream.cuda_stream))
         elif kern == "pfit":
@@ -100,7 +103,7 @@ def main():
     res = {}
     for name, *rest in variants:
         ms = np.array([a.elapsed_time(b) for a, b in times[name]])
-        byts = 4.0 * P * N if name.startswith("probe_read") else alg
+        byts = 4.0 * P * N if name.startswith("probe_read") else (4.0 * P * k if name.startswith("probe_write") else alg)
         res[name] = {"median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
                      "GBps_median": byts / (np.median(ms) * 1e-3) / 1e9}
         print(f"{name:24s} median {np.median(ms):.4f} ms  min {ms.min():.4f} ms  "
