@@ -159,6 +159,19 @@ int rti_apply_operator(const float* opT, int E, int N, int64_t op_stride,
                        void* out, int out_dtype, int64_t out_row_stride, int64_t out_channel_stride,
                        rti_stream_t stream);
 
+/* ---- device: per-pixel linear RBF (the reference's default, with its own geometry) ---
+ * interpolate_intensities (analysis.py:350-363) -> _interpolate_RBF (analysis.py:249-260)
+ * for every pixel: nodes x_n = (lu[p][n], lv[p][n]) and values I[p][n], PIXEL-major as
+ * compute_intensities returns them; A_ij = ‖x_i − x_j‖, A w = I solved in fp64 by LU with
+ * partial pivoting, f(q_e) = Σ_n w_n ‖q_e − x_n‖ evaluated in fp64 at luv[E][2] (device).
+ * out: F64 / F32 / I32 / U8, layout RTI_OUT_PIXEL_MAJOR ([p][e], the reference's
+ * [y][x][ly][lx]) or RTI_OUT_EVAL_MAJOR ([e][p], prepare_images_data's [ly][lx][y][x]).
+ * status: device int the caller zeroes; set to RTI_ERR_SINGULAR when a pixel's system is
+ * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 128. */
+int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
+                     const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
+                     rti_stream_t stream);
+
 /* ---- device: light vectors ---------------------------------------------------------
  * The light-vector half of compute_intensities (analysis.py:221-231) for an
  * H×W ROI and N cameras: lu[p][n], lv[p][n] (fp32, pixel-major, p = y*W + x),

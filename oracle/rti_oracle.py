@@ -307,6 +307,49 @@ def relight(coef, basis, lu, lv):
 
 
 # ----------------------------------------------------------------------------
+# Linear RBF (analysis.py:249-260: SciPy Rbf(x, y, I, function='linear'))
+# ----------------------------------------------------------------------------
+def rbf_linear(x_coarse, y_coarse, intensity_values, x_fine, y_fine):
+    """Restates SciPy's Rbf with function='linear', smooth=0, norm='euclidean' as the
+    reference calls it (analysis.py:259-260): nodes are float64 copies of the float32
+    light vectors, A_ij = ‖x_i − x_j‖, w = solve(A, I) (LU with partial pivoting; a
+    singular A raises numpy.linalg.LinAlgError like SciPy's LinAlgError), and
+    f(q) = Σ_j w_j ‖q − x_j‖ (cdist · nodes)."""
+    X = np.stack([np.asarray(x_coarse, np.float64).ravel(), np.asarray(y_coarse, np.float64).ravel()], -1)
+    A = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    w = np.linalg.solve(A, np.asarray(intensity_values, np.float64).ravel())
+    xf = np.asarray(x_fine, np.float64)
+    Q = np.stack([xf.ravel(), np.asarray(y_fine, np.float64).ravel()], -1)
+    D = np.sqrt(((Q[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    return (D @ w).reshape(xf.shape)
+
+
+def rbf_operator(lu, lv, qu, qv):
+    """Shared-node linear-RBF operator opT[N, E] with out = opTᵀ · I (M = Φ A⁻¹, fp64)."""
+    X = np.stack([np.asarray(lu, np.float64), np.asarray(lv, np.float64)], -1)
+    A = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    Q = np.stack([np.asarray(qu, np.float64), np.asarray(qv, np.float64)], -1)
+    Phi = np.sqrt(((Q[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    return np.linalg.solve(A, Phi.T)  # A symmetric: A⁻¹ Φᵀ = (Φ A⁻¹)ᵀ
+
+
+def interpolate_intensities_rbf(data):
+    """RBF (default) branch of interpolate_intensities (analysis.py:321-372) -> [R, R, G, G] f64."""
+    if data is None or len(data) != 3:
+        raise Exception("Error computing interpolation: results are empty or invalid")
+    lx, ly, inten = data
+    R = lx.shape[0]
+    _, xi = np.mgrid[-1:1:INTERPOLATION_PARAM, -1:1:INTERPOLATION_PARAM]
+    yi, _ = np.mgrid[-1:1:INTERPOLATION_PARAM, -1:1:INTERPOLATION_PARAM]
+    xi, yi = np.around(xi, 2), np.around(yi, 2)
+    out = np.empty((R, R) + xi.shape)
+    for y in range(R):
+        for x in range(R):
+            out[y, x] = rbf_linear(lx[y][x], ly[y][x], inten[y][x], xi, yi)
+    return out
+
+
+# ----------------------------------------------------------------------------
 # Relight lookup (interactive_relighting.py:11-39, Utils/utilities.py:357-381)
 # ----------------------------------------------------------------------------
 def draw_light_roi_position(given_x, given_y, shape, to_light_vector=False):

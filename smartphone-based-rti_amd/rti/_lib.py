@@ -84,6 +84,8 @@ SIGNATURES = {
                                     _c_double_p]),
     "rti_apply_operator": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_void_p, _c_int, _c_i64, _c_int, _c_i64,
                                     _c_i64, _c_void_p, _c_int, _c_i64, _c_i64, _c_void_p]),
+    "rti_rbf_perpixel": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_i64, _c_void_p, _c_int,
+                                  _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p]),
     "rti_relight": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_int, _c_void_p, _c_int, _c_void_p, _c_int,
                              _c_int, _c_void_p]),
 }

@@ -353,3 +353,36 @@ def apply_operator(opT, I, out_dtype=torch.float32):
 def interpolate_rbf(I, lu, lv, qu, qv, out_dtype=torch.float32):
     """Linear-RBF interpolation of every pixel at (qu, qv) for a SHARED light set -> [.., E, H, W]."""
     return apply_operator(rbf_operator(lu, lv, qu, qv), I, out_dtype=out_dtype)
+
+
+def interpolate_rbf_perpixel(I, lu, lv, qu, qv, out_dtype=torch.float64, out_layout="pixel"):
+    """Per-pixel linear RBF (the reference's default with per-pixel light lists) on the GPU.
+
+    I, lu, lv: pixel-major [.., N] (compute_intensities' layout), on any device.
+    Returns [.., E] (out_layout="pixel") or [E, ..] ("eval").  Raises
+    numpy.linalg.LinAlgError if any pixel's system is singular, as SciPy does."""
+    _require_cuda(I, "I")
+    dev = I.device
+    odt = _OUT_DTYPES.get(out_dtype)
+    if odt is None:
+        raise ValueError("out_dtype must be float32, float64, int32 or uint8")
+    lu_d = torch.as_tensor(lu, device=dev).to(torch.float32).contiguous()
+    lv_d = torch.as_tensor(lv, device=dev).to(torch.float32).contiguous()
+    if lu_d.shape != I.shape or lv_d.shape != I.shape:
+        raise ValueError("per-pixel lu, lv and I must share the pixel-major shape [.., N]")
+    N = I.shape[-1]
+    spatial = tuple(I.shape[:-1])
+    P = int(np.prod(spatial)) if spatial else 1
+    qu, qv = _query(qu, qv)
+    luv = torch.as_tensor(np.ascontiguousarray(np.stack([qu, qv], -1)), device=dev)
+    E = qu.size
+    ol = L.RTI_OUT_PIXEL_MAJOR if out_layout == "pixel" else L.RTI_OUT_EVAL_MAJOR
+    out = torch.empty(spatial + (E,) if ol == L.RTI_OUT_PIXEL_MAJOR else (E,) + spatial, dtype=out_dtype, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    Ic = I.contiguous()
+    st = L.lib().rti_rbf_perpixel(_vp(lu_d), _vp(lv_d), _vp(Ic), _IN_DTYPES[Ic.dtype], N, P, _vp(luv), E, _vp(out),
+                                  odt, ol, _vp(status), _stream_of(I))
+    L.check(st, "rti_rbf_perpixel")
+    if int(status.item()) == L.RTI_ERR_SINGULAR:
+        raise np.linalg.LinAlgError("Matrix is singular.")
+    return out

@@ -10,7 +10,7 @@ compute_intensities             analysis.py:196-246                          rti
 _interpolate_PTM                analysis.py:263-317                          rti_fit_perpixel_dirs (P=1) + rti_relight
 _interpolate_RBF                analysis.py:249-260                          rti_rbf_operator + rti_apply_operator
 interpolate_intensities (PTM)   analysis.py:321-372                          rti_fit_perpixel_dirs + rti_relight (pixel-major)
-interpolate_intensities (RBF)   analysis.py:321-372 (default method)         rti_rbf_operator + rti_apply_operator
+interpolate_intensities (RBF)   analysis.py:321-372 (default method)         rti_rbf_perpixel, or the shared operator
 prepare_images_data             analysis.py:375-411                          layout adapter (torch); native: relight_tables
 relighting_event lookup         interactive_relighting.py:11-39              table lookup + clip (host, one image)
 ==============================  ===========================================  ==============================
@@ -20,10 +20,9 @@ arrays with the reference's dtypes.  The reference returns nested lists; here
 the same indexing ([y][x][ly][lx], [ly][lx][y][x]) works on ndarrays.
 Differences, by design:
   * the ROI size is the data's size, not ``constants.ROI_DIAMETER``;
-  * the RBF branch (``interpolate_PTM=False``, the reference's default) runs
-    when every pixel sees the same light directions (directional lights: one
-    shared operator); per-pixel light lists with RBF raise ``NotImplementedError``
-    for now;
+  * the RBF branch (``interpolate_PTM=False``, the reference's default) uses one
+    shared operator when every pixel sees the same light directions, else one
+    fp64 LU solve per pixel (rti_rbf_perpixel);
   * the debug plots of ``first_only=True`` are not drawn (first pixel only is kept).
 """
 from __future__ import annotations
@@ -135,13 +134,18 @@ def interpolate_intensities(data, interpolate_PTM=False, first_only=False, devic
 
 
 def _interpolate_rbf_roi(lx, ly, inten, device):
-    """RBF branch of interpolate_intensities (analysis.py:360-363) for a shared light list."""
-    if not _shared_directions(lx, ly):
-        raise NotImplementedError("linear RBF with per-pixel light directions is not implemented yet; "
-                                  "directional (shared) light lists run on the GPU operator path")
+    """RBF branch of interpolate_intensities (analysis.py:360-363).
+
+    Shared light list (directional lights): one operator for all pixels (MFMA).
+    Per-pixel light lists (the reference's geometry): one fp64 solve per pixel."""
     dev = _device(device)
     R, N = lx.shape[0], lx.shape[-1]
     G, qu, qv = _grid_luv(grid_axis())
+    if not _shared_directions(lx, ly):
+        it = inten if inten.dtype in (np.float32, np.int32, np.uint8) else inten.astype(np.int32)
+        I = torch.as_tensor(np.ascontiguousarray(it), device=dev)
+        out = api.interpolate_rbf_perpixel(I, lx, ly, qu, qv, out_dtype=torch.float64)
+        return out.reshape(R, R, G, G).cpu().numpy()
     op = api.rbf_operator(lx[0, 0], ly[0, 0], qu, qv)
     it = inten if inten.dtype in (np.float32, np.int32, np.uint8) else inten.astype(np.int32)
     I = torch.as_tensor(np.ascontiguousarray(it.reshape(R * R, N).T), device=dev)  # light-major [N, P]

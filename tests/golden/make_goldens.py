@@ -197,6 +197,34 @@ def gen_rbf(analysis, out, n=20, npx=4, seed=3):
                         meta=meta())
 
 
+def gen_rbf_perpixel(analysis, out, roi=4, seed=5):
+    """The reference's DEFAULT path: interpolate_intensities(interpolate_PTM=False) on per-pixel
+    light vectors from compute_intensities, then prepare_images_data."""
+    p = np.load(os.path.join(out, "ptm_perpixel_32x32_N50.npz"))
+    lx, ly, inten = p["lx"][:roi, :roi], p["ly"][:roi, :roi], p["I"][:roi, :roi]
+    analysis.cst.ROI_DIAMETER = roi
+    try:
+        grid = np.array(quiet(analysis.interpolate_intensities, (lx, ly, inten), interpolate_PTM=False))
+        tables = np.array(quiet(analysis.prepare_images_data, grid))
+    finally:
+        analysis.cst.ROI_DIAMETER = 400
+    # a repeated light direction makes SciPy's linear system singular
+    lx2 = lx[:1, :1].copy()
+    ly2 = ly[:1, :1].copy()
+    lx2[0, 0, 1], ly2[0, 0, 1] = lx2[0, 0, 0], ly2[0, 0, 0]
+    analysis.cst.ROI_DIAMETER = 1
+    try:
+        quiet(analysis.interpolate_intensities, (lx2, ly2, inten[:1, :1]), interpolate_PTM=False)
+        raised = ""
+    except Exception as e:
+        raised = type(e).__name__
+    finally:
+        analysis.cst.ROI_DIAMETER = 400
+    np.savez_compressed(os.path.join(out, f"rbf_perpixel_{roi}x{roi}_N{lx.shape[-1]}.npz"), lx=lx, ly=ly, I=inten,
+                        grid=grid, tables=tables, singular_lx=lx2, singular_ly=ly2, singular_raises=np.array(raised),
+                        meta=meta())
+
+
 def gen_lookup(utilities, out, seed=4):
     """Cursor -> (lx, ly) -> table index (Utils/utilities.py:357-381, interactive_relighting.py:25-26)."""
     rng = np.random.default_rng(seed)
@@ -227,6 +255,7 @@ def main():
         "perpixel": lambda: gen_perpixel(analysis, args.out),
         "edge": lambda: gen_edge(analysis, args.out),
         "rbf": lambda: gen_rbf(analysis, args.out),
+        "rbf_perpixel": lambda: gen_rbf_perpixel(analysis, args.out),
         "lookup": lambda: gen_lookup(utilities, args.out),
     }
     for name, job in jobs.items():

@@ -59,10 +59,7 @@ def test_compat_interpolate_intensities_default_rbf(cuda):
     fused = compat.rbf_tables(torch.as_tensor(np.ascontiguousarray(d["I"].T.reshape(N, 2, 2)), device=cuda),
                               d["lu"], d["lv"]).cpu().numpy()
     assert not ((fused != ref_t) & ~near).any()
-    lx2 = lx.copy()
-    lx2[1, 1, 0] += 0.01
-    with pytest.raises(NotImplementedError):
-        compat.interpolate_intensities((lx2, ly, inten))
+
 
 
 def test_rbf_singular_raises_linalgerror(cuda):
@@ -104,3 +101,43 @@ def test_operator_channels_and_int_outputs(cuda):
     frac = np.abs(ref - np.round(ref)) > 1e-3
     assert np.array_equal(i32[frac], np.trunc(ref[frac]).astype(np.int32))
     assert np.array_equal(u8[frac], np.clip(np.trunc(ref[frac]), 0, 255).astype(np.uint8))
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float64, torch.float32])
+def test_rbf_perpixel_matches_reference_default_path(cuda, out_dtype):
+    d = golden("rbf_perpixel_4x4_N50.npz")
+    I = torch.as_tensor(d["I"], device=cuda)
+    qu, qv = grid_q()
+    out = rti.interpolate_rbf_perpixel(I, d["lx"], d["ly"], qu, qv, out_dtype=out_dtype).cpu().numpy()
+    err, ok = relight_close(out.reshape(4, 4, 100, 100), d["grid"], rtol=1e-9 if out_dtype == torch.float64 else 1e-6)
+    assert ok, err
+    ev = rti.interpolate_rbf_perpixel(I, d["lx"], d["ly"], qu, qv, out_dtype=torch.int32, out_layout="eval")
+    near = np.abs(d["grid"] - np.round(d["grid"])) < 1e-6
+    t = ev.cpu().numpy().reshape(100, 100, 4, 4)
+    assert not ((t != d["tables"]) & ~np.transpose(near, (2, 3, 0, 1))).any()
+
+
+def test_compat_default_interpolation_perpixel(cuda):
+    d = golden("rbf_perpixel_4x4_N50.npz")
+    grid = compat.interpolate_intensities((d["lx"], d["ly"], d["I"]))  # interpolate_PTM=False: the default
+    assert grid.shape == (4, 4, 100, 100) and grid.dtype == np.float64
+    err, ok = relight_close(grid, d["grid"], rtol=1e-9)
+    assert ok, err
+    one = compat.interpolate_intensities((d["lx"], d["ly"], d["I"]), first_only=True)
+    assert one.shape == (1, 1, 100, 100)
+    with pytest.raises(np.linalg.LinAlgError):
+        compat.interpolate_intensities((d["singular_lx"], d["singular_ly"], d["I"][:1, :1]))
+
+
+@pytest.mark.parametrize("n", [6, 37, 64, 65, 100, 128])
+def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
+    ys, xs = np.mgrid[0:3, 0:5]
+    rng = np.random.default_rng(n)
+    cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
+    lu, lv = o.light_dirs_for_pixels(cams, xs.ravel(), ys.ravel())  # [15, n] float32
+    inten = rng.integers(0, 256, (15, n)).astype(np.int32)
+    qu, qv = rng.uniform(-1, 1, 300), rng.uniform(-1, 1, 300)
+    out = rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv).cpu().numpy()
+    ref = np.stack([o.rbf_linear(lu[p], lv[p], inten[p], qu, qv) for p in range(15)])
+    err, ok = relight_close(out, ref, rtol=1e-8)
+    assert ok, err

@@ -146,8 +146,6 @@ def test_compat_interpolate_and_prepare(cuda):
     assert np.array_equal(compat.prepare_images_data(d["grid"]), ref_t)
     one = compat.interpolate_intensities(data, interpolate_PTM=True, first_only=True)
     assert one.shape == (1, 1, 100, 100)
-    with pytest.raises(NotImplementedError):
-        compat.interpolate_intensities(data)
     with pytest.raises(Exception, match="empty or invalid"):
         compat.interpolate_intensities((1, 2), interpolate_PTM=True)
 

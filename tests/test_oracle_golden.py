@@ -107,3 +107,26 @@ def test_hsh_basis_is_orthonormal_on_hemisphere():
     w = (np.sin(T) * (np.pi / 2 / n_t) * (2 * np.pi / n_p)).ravel()
     G = (B * w[:, None]).T @ B
     assert np.allclose(G, np.eye(16), atol=2e-3)
+
+
+def test_rbf_restatement_matches_scipy_goldens():
+    d = golden("rbf_shared_4px_N20.npz")
+    yi, xi = np.mgrid[-1:1:0.02, -1:1:0.02]
+    xi, yi = np.around(xi, 2), np.around(yi, 2)
+    for p in range(4):
+        g = o.rbf_linear(d["lu"], d["lv"], d["I"][p], xi, yi)
+        assert np.abs(g - d["grid"][p]).max() < 1e-9
+    op = o.rbf_operator(d["lu"], d["lv"], xi.ravel(), yi.ravel())
+    assert np.abs((op.T @ d["I"].T.astype(np.float64)).T.reshape(-1, 100, 100) - d["grid"]).max() < 1e-9
+
+
+def test_rbf_perpixel_default_path_matches_reference():
+    d = golden("rbf_perpixel_4x4_N50.npz")
+    grid = o.interpolate_intensities_rbf((d["lx"], d["ly"], d["I"]))
+    assert np.abs(grid - d["grid"]).max() < 1e-8
+    t = o.prepare_images_data(grid)
+    near = np.abs(d["grid"] - np.round(d["grid"])) < 1e-6
+    assert not ((t != d["tables"]) & ~np.transpose(near, (2, 3, 0, 1))).any()
+    assert str(d["singular_raises"]) == "LinAlgError"
+    with pytest.raises(np.linalg.LinAlgError):
+        o.rbf_linear(d["singular_lx"][0, 0], d["singular_ly"][0, 0], d["I"][0, 0], [0.0], [0.0])
