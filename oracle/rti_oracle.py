@@ -312,12 +312,14 @@ def relight(coef, basis, lu, lv):
 def rbf_linear(x_coarse, y_coarse, intensity_values, x_fine, y_fine):
     """Restates SciPy's Rbf with function='linear', smooth=0, norm='euclidean' as the
     reference calls it (analysis.py:259-260): nodes are float64 copies of the float32
-    light vectors, A_ij = ‖x_i − x_j‖, w = solve(A, I) (LU with partial pivoting; a
-    singular A raises numpy.linalg.LinAlgError like SciPy's LinAlgError), and
+    light vectors, A_ij = ‖x_i − x_j‖, w = scipy.linalg.solve(A, I) (LU with partial
+    pivoting; an exactly singular A raises LinAlgError), and
     f(q) = Σ_j w_j ‖q − x_j‖ (cdist · nodes)."""
+    import scipy.linalg  # the solver SciPy's Rbf itself uses (LAPACK gesv)
+
     X = np.stack([np.asarray(x_coarse, np.float64).ravel(), np.asarray(y_coarse, np.float64).ravel()], -1)
     A = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
-    w = np.linalg.solve(A, np.asarray(intensity_values, np.float64).ravel())
+    w = scipy.linalg.solve(A, np.asarray(intensity_values, np.float64).ravel())
     xf = np.asarray(x_fine, np.float64)
     Q = np.stack([xf.ravel(), np.asarray(y_fine, np.float64).ravel()], -1)
     D = np.sqrt(((Q[:, None, :] - X[None, :, :]) ** 2).sum(-1))
