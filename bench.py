@@ -43,6 +43,9 @@ CONFIGS = {
     "c7": ("operator", 400, 400, 100, 1, "rbf",
            "linear-RBF interpolation (reference default, SciPy Rbf) of a 400x400 ROI x 100 shared lights on the "
            "100x100 grid -> int32 tables (interpolate_intensities + prepare_images_data)"),
+    "c8": ("rbf_perpixel", 400, 400, 100, 1, "rbf",
+           "reference default pipeline: per-pixel linear RBF (own light list per pixel, fp64 LU) of a 400x400 ROI x "
+           "100 lights on the 100x100 grid -> int32 tables"),
 }
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
 
@@ -344,8 +347,80 @@ class OperatorWorkload:
                           f"evals, {reps} reps in {el:.1f}s; {name}"}
 
 
+class RbfPerPixelWorkload:
+    """One step = one rti_rbf_perpixel launch over the ROI: per-pixel fp64 solve + 10^4 evaluations."""
+
+    def __init__(self, args, cfg, rank, dev):
+        import rti
+
+        self.rti = rti
+        _, H, W, N, C, basis, desc = cfg
+        self.H, self.W, self.N, self.desc = H, W, N, desc
+        self.P = P = H * W
+        cams = synth_cams(N, 6, H, W)
+        ys, xs = np.divmod(np.arange(P), W)
+        dx = cams[None, :, 0] - xs[:, None]
+        dy = cams[None, :, 1] - ys[:, None]
+        nrm = np.sqrt(dx * dx + dy * dy + cams[None, :, 2] ** 2)
+        self.lu_h = (dx / nrm).astype(np.float32)
+        self.lv_h = (dy / nrm).astype(np.float32)
+        self.lu = torch.as_tensor(self.lu_h, device=dev)
+        self.lv = torch.as_tensor(self.lv_h, device=dev)
+        rng = np.random.default_rng(7 + rank)
+        self.I_h = rng.integers(0, 256, (P, N)).astype(np.int32)
+        self.I = torch.as_tensor(self.I_h, device=dev)
+        xf = np.around(np.mgrid[-1:1:0.02, -1:1:0.02][1], 2)[0]
+        self.qu, self.qv = np.tile(xf, xf.size), np.repeat(xf, xf.size)
+        self.E = E = self.qu.size
+        self.luv = torch.as_tensor(np.stack([self.qu, self.qv], -1), device=dev).contiguous()
+        self.out = torch.empty((E, P), dtype=torch.int32, device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.units = P * E
+        self.alg_bytes = 12.0 * P * N + 4.0 * P * E
+        self.flops = P * (2.0 / 3.0 * N ** 3 + 5.0 * N * N + 8.0 * N * E)  # LU + A build + evaluation (fp64)
+        self.metric = f"Mpix*evals/sec {desc}"
+        self.unit = "Mpix*evals/s"
+        import ctypes
+
+        self.ctypes = ctypes
+        self.lib = rti._lib.lib()
+
+    def step(self, i):
+        c = self.ctypes
+        L = self.rti._lib
+        st = self.lib.rti_rbf_perpixel(c.c_void_p(self.lu.data_ptr()), c.c_void_p(self.lv.data_ptr()),
+                                       c.c_void_p(self.I.data_ptr()), L.RTI_I32, self.N, self.P,
+                                       c.c_void_p(self.luv.data_ptr()), self.E, c.c_void_p(self.out.data_ptr()),
+                                       L.RTI_I32, L.RTI_OUT_EVAL_MAJOR, c.c_void_p(self.status.data_ptr()),
+                                       c.c_void_p(torch.cuda.current_stream().cuda_stream))
+        L.check(st, "rti_rbf_perpixel")
+
+    def config(self):
+        return {"lights": self.N, "evals": self.E, "basis": "rbf-linear per-pixel", "out": "int32 tables [E][P]"}
+
+    def roofline(self, kernel_ms):
+        ach = self.flops / (kernel_ms * 1e-3) / 1e12
+        return {"bound": "fp64-valu", "achieved": round(ach, 2), "peak": 78.6, "unit": "TFLOP/s",
+                "frac": round(ach / 78.6, 4), "traffic": None, "kernel_ms": round(kernel_ms, 4),
+                "alg_flops_per_launch": self.flops, "alg_bytes_per_launch": self.alg_bytes}
+
+    def cpu_baseline(self, budget_s):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import rti_oracle as o
+
+        npx = 16
+        def run():
+            for p in range(npx):
+                o.rbf_linear(self.lu_h[p], self.lv_h[p], self.I_h[p], self.qu, self.qv)
+        rate, reps, el = cpu_sample_rate(run, npx * self.E, budget_s)
+        threads, name = cpu_info()
+        return {"value": round(rate, 3), "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oracle rbf_linear (SciPy-equivalent fp64 solve + cdist eval) on {npx} px x {self.E} "
+                          f"evals, {reps} reps in {el:.1f}s; {name}"}
+
+
 WORKLOADS = {"fit": FitWorkload, "relight": RelightWorkload, "perpixel": PerPixelWorkload,
-             "operator": OperatorWorkload}
+             "operator": OperatorWorkload, "rbf_perpixel": RbfPerPixelWorkload}
 
 
 def main():
@@ -366,7 +441,7 @@ def main():
     cfg = CONFIGS[args.config]
     kind = cfg[0]
     if args.steps is None:
-        args.steps = {"fit": 20, "relight": 1000, "perpixel": 10, "operator": 10}[kind]
+        args.steps = {"fit": 20, "relight": 1000, "perpixel": 10, "operator": 10, "rbf_perpixel": 3}[kind]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -454,7 +529,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": {"perpixel": "f32 in / f64 solve", "operator": "f32 (MFMA) -> int32"}.get(kind, "f32"),
+            "dtype": {"perpixel": "f32 in / f64 solve", "operator": "f32 (MFMA) -> int32",
+                      "rbf_perpixel": "f64 -> int32"}.get(kind, "f32"),
             "data": "synthetic (seeded smooth PTM/HSH coefficient fields + N(0,2) noise, rounded to 0..255, fp32)",
             "config": conf,
             "roofline": wl.roofline(kernel_ms) if hasattr(wl, "roofline") else {
