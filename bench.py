@@ -150,11 +150,15 @@ class FitWorkload:
         self.args = args
         self.lu, self.lv = synth_dirs(N, seed=2)
         self.I = synth_stack(H, W, N, C, basis, self.lu, self.lv, seed=1000 + rank, device=dev)
+        self.in_bytes = 4
+        if args.in_dtype != "f32":  # integer-valued 0..255 stacks, as the reference's V channel (analysis.py:219)
+            self.I = self.I.to(torch.uint8 if args.in_dtype == "u8" else torch.int32)
+            self.in_bytes = 1 if args.in_dtype == "u8" else 4
         self.pinv64 = rti.pinv(self.lu, self.lv, basis)
         self.pinv_dev = torch.as_tensor(self.pinv64.astype(np.float32), device=dev)
         self.coef = torch.empty((C, P, k) if args.layout == "pixel" else (C, k, P), dtype=torch.float32, device=dev)
         self.units = P * N * C
-        self.alg_bytes = 4.0 * P * N * C + 4.0 * P * k * C  # fp32 stack read once + fp32 coefficients written
+        self.alg_bytes = float(self.in_bytes) * P * N * C + 4.0 * P * k * C  # stack read once + fp32 coefs written
         self.metric = "Mpix*lights/sec PTM fit (4K, 100 lights)" if args.config == "c3" else f"Mpix*lights/sec {desc}"
         self.unit = "Mpix*lights/s"
 
@@ -164,7 +168,7 @@ class FitWorkload:
 
     def config(self):
         return {"lights": self.N, "channels": self.C, "basis": self.basis, "k": self.k,
-                "coef_layout": self.args.layout, "kernel": self.args.kernel}
+                "coef_layout": self.args.layout, "kernel": self.args.kernel, "intensity_dtype": self.args.in_dtype}
 
     def cpu_baseline(self, budget_s):
         """Oracle restatement: fp64 pinv + fp32 NumPy matmul on light-major rows."""
@@ -172,7 +176,7 @@ class FitWorkload:
         import rti_oracle as o
 
         rows = max(1, self.H // 10)
-        sample = self.I[0, :, : rows * self.W].cpu().numpy()
+        sample = self.I[0, :, : rows * self.W].float().cpu().numpy()
         rate, reps, el = cpu_sample_rate(lambda: o.fit_shared_f32(sample, self.pinv64), self.N * rows * self.W,
                                          budget_s)
         threads, name = cpu_info()
@@ -432,6 +436,8 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma"])
     ap.add_argument("--layout", default="pixel", choices=["pixel", "planar"])
     ap.add_argument("--nontemporal", action="store_true")
+    ap.add_argument("--in-dtype", default="f32", choices=["f32", "u8", "i32"],
+                    help="intensity stack type for fit configs (BASELINE's metric is fp32)")
     ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of the maps")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -530,7 +536,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": {"perpixel": "f32 in / f64 solve", "operator": "f32 (MFMA) -> int32",
-                      "rbf_perpixel": "f64 -> int32"}.get(kind, "f32"),
+                      "rbf_perpixel": "f64 -> int32"}.get(kind, "f32" if args.in_dtype == "f32"
+                                                          else f"{args.in_dtype} in / f32 compute"),
             "data": "synthetic (seeded smooth PTM/HSH coefficient fields + N(0,2) noise, rounded to 0..255, fp32)",
             "config": conf,
             "roofline": wl.roofline(kernel_ms) if hasattr(wl, "roofline") else {

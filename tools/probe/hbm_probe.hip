@@ -220,3 +220,77 @@ extern "C" int probe_write(float* out, int64_t bytes, void* stream) {
   hipLaunchKernelGGL(write_stream, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out, n4);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// Soft phase separation: persistent workgroups (contiguous tile ranges) buffer F tiles of
+// coefficients in LDS and flush them as 1 KiB-per-wave-instruction bursts.
+template <int F>
+__global__ void __launch_bounds__(256) fit6_persist(const float* __restrict__ pinv, const float* __restrict__ I, int N,
+                                                    int64_t P, float* __restrict__ coef, int tiles_per_wg) {
+  extern __shared__ __attribute__((aligned(16))) float buf[];  // [F][1024 px][6]
+  const int64_t ntiles = P / 1024;
+  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_wg;
+  const int64_t t1 = t0 + tiles_per_wg < ntiles ? t0 + tiles_per_wg : ntiles;
+  int pending = 0;
+  int64_t first = t0;
+  for (int64_t t = t0; t < t1; ++t) {
+    const int64_t p0 = t * 1024 + threadIdx.x * 4;
+    float acc[6][4] = {};
+    const float* src = I + p0;
+    int n = 0;
+    for (; n + 8 <= N; n += 8) {
+      floatx4 x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = ld4<true>(src + (int64_t)(n + u) * P);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const float w = pinv[k * N + n + u];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[k][v] = fmaf(w, x[u][v], acc[k][v]);
+        }
+    }
+    for (; n < N; ++n) {
+      floatx4 x = ld4<true>(src + (int64_t)n * P);
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[k][v] = fmaf(pinv[k * N + n], x[v], acc[k][v]);
+    }
+    float* slot = buf + pending * 1024 * 6 + threadIdx.x * 24;
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int k = 0; k < 6; k += 2) *reinterpret_cast<float2*>(slot + v * 6 + k) = float2{acc[k][v], acc[k + 1][v]};
+    ++pending;
+    if (pending == F || t + 1 == t1) {
+      __syncthreads();
+      const int nf = pending * 1024 * 6 / 4;  // float4s to flush (contiguous in global)
+      float* dst = coef + first * 1024 * 6;
+      for (int i = threadIdx.x; i < nf; i += 256)
+        reinterpret_cast<floatx4*>(dst)[i] = reinterpret_cast<const floatx4*>(buf)[i];
+      __syncthreads();
+      pending = 0;
+      first = t + 1;
+    }
+  }
+}
+
+extern "C" int probe_persist(const float* pinv, const float* I, int N, int64_t P, float* coef, int variant,
+                             void* stream) {
+  // variant = F * 1000 + workgroups (e.g. 3512 = flush every 3 tiles, 512 workgroups)
+  const int F = variant / 1000, wgs = variant % 1000;
+  const int64_t ntiles = P / 1024;
+  const int per = (int)((ntiles + wgs - 1) / wgs);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = (size_t)F * 1024 * 6 * 4;
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fit6_persist<3>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  switch (F) {
+    case 1: hipLaunchKernelGGL(fit6_persist<1>, dim3(wgs), dim3(256), lds, s, pinv, I, N, P, coef, per); break;
+    case 2: hipLaunchKernelGGL(fit6_persist<2>, dim3(wgs), dim3(256), lds, s, pinv, I, N, P, coef, per); break;
+    default: hipLaunchKernelGGL(fit6_persist<3>, dim3(wgs), dim3(256), lds, s, pinv, I, N, P, coef, per); break;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}

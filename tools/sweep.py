@@ -66,8 +66,11 @@ def main():
         if k == 6:
             for pvnt, nm in ((1, "nostore"),):
                 variants.append((f"probe_fit6_{nm}", "pfit", str(pvnt), 0))
-            for pvnt, nm in ((0, "plain"), (5, "planar"), (7, "plain_xcd"), (8, "planar_xcd"), (4, "win64K")):
+            for pvnt, nm in ((0, "plain"), (4, "win64K")):
                 variants.append((f"probe_store_{nm}", "pstore", str(pvnt), 0))
+            probe.probe_persist.argtypes = probe.probe_fit6.argtypes
+            for v in (1256, 1512, 2256, 2512, 3256, 1768, 2384):
+                variants.append((f"probe_persist_F{v // 1000}_wg{v % 1000}", "ppersist", str(v), 0))
     stream = torch.cuda.current_stream(dev)
     times = {name: [] for name, *_ in variants}
 
@@ -77,6 +80,10 @@ def main():
                              ctypes.c_void_p(stream.cuda_stream))
         elif kern == "pwrite":
             probe.probe_write(ctypes.c_void_p(coefs["pixel"].data_ptr()), 4 * P * k, ctypes.c_void_p(stream.cuda_stream))
+        elif kern == "ppersist":
+            probe.probe_persist(ctypes.c_void_p(pv.data_ptr()), ctypes.c_void_p(I.data_ptr()), N, P,
+                                ctypes.c_void_p(coefs["pixel"].data_ptr()), int(layout),
+                                ctypes.c_void_p(stream.cuda_stream))
         elif kern == "pstore":
             tgt = coefs["planar"] if layout in ("5", "8") else coefs["pixel"]
             probe.probe_store(ctypes.c_void_p(pv.data_ptr()), ctypes.c_void_p(I.data_ptr()), N, P,
