@@ -516,7 +516,7 @@ def main():
 
     value = world * wl.units * args.steps / elapsed / 1e6
     achieved = wl.alg_bytes / (kernel_ms * 1e-3) / 1e9
-    workload_key = f"{args.config}-{args.kernel}-{args.layout}"
+    workload_key = f"{args.config}-{args.kernel}-{args.layout}" + ("" if args.in_dtype == "f32" else f"-{args.in_dtype}")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = wl.cpu_baseline(args.cpu_budget)

@@ -13,6 +13,7 @@ interpolate_intensities (PTM)   analysis.py:321-372                          rti
 interpolate_intensities (RBF)   analysis.py:321-372 (default method)         rti_rbf_perpixel, or the shared operator
 prepare_images_data             analysis.py:375-411                          layout adapter (torch); native: relight_tables
 relighting_event lookup         interactive_relighting.py:11-39              table lookup + clip (host, one image)
+compute (steps 2-4 + save)      analysis.py:414-482 (from_storage=True)      compute_tables: fused GPU pipeline
 ==============================  ===========================================  ==============================
 
 Inputs may be NumPy arrays (as in the reference) or tensors; outputs are NumPy
@@ -26,6 +27,8 @@ Differences, by design:
   * the debug plots of ``first_only=True`` are not drawn (first pixel only is kept).
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -220,3 +223,48 @@ def relight_at_cursor(coef, x, y, shape, basis="ptm"):
     """Continuous relighting: cursor -> (lx, ly) -> uint8 V image from coefficients."""
     lx, ly = draw_light_roi_position(x, y, shape, to_light_vector=True)
     return api.relight(coef, lx, ly, basis=basis, out_dtype=torch.uint8)
+
+
+def compute_tables(results_frames, interpolate_PTM=False, first_only=False, origin=(0.0, 0.0), device=None):
+    """Steps 2-4 of analysis.compute (analysis.py:465-472) fused on the GPU.
+
+    results_frames: the reference's list of (V uint8[R,R], camera f64[3]).  Returns the
+    int32 tables [G, G, R, R] ([ly][lx][y][x]) that prepare_images_data would produce.
+    PTM: light vectors + per-pixel fit in one kernel, then the 100×100 grid in one relight
+    launch (fp64, reference op order).  RBF (the default): light vectors, then one
+    per-pixel fp64 solve + evaluation launch writing the tables directly."""
+    if results_frames is None or len(results_frames) <= 0:
+        raise Exception("Error computing intensities: results are empty")
+    dev = _device(device)
+    frames = np.stack([np.asarray(f) for f, _ in results_frames])
+    cams = np.stack([np.asarray(c, np.float64).ravel()[:3] for _, c in results_frames])
+    R = 1 if first_only else frames.shape[1]
+    frames = np.ascontiguousarray(frames[:, :R, :R])
+    G, qu, qv = _grid_luv(grid_axis())
+    if interpolate_PTM:
+        I = torch.as_tensor(frames, device=dev)  # light-major [N, R, R] uint8
+        coef = api.fit(I, cams=cams, origin=origin, mode="perpixel", coef_dtype=torch.float64)
+        out = api.relight(coef, qu, qv, basis="ptm", out_dtype=torch.int32, out_layout="eval")
+    else:
+        lu, lv = api.light_dirs(cams, R, R, origin=origin, device=dev)
+        I = torch.as_tensor(np.ascontiguousarray(np.moveaxis(frames, 0, -1)), device=dev)  # [R, R, N]
+        out = api.interpolate_rbf_perpixel(I, lu, lv, qu, qv, out_dtype=torch.int32, out_layout="eval")
+    return out.reshape(G, G, R, R).cpu().numpy()
+
+
+def compute(video_name="coin1", from_storage=True, storage_filepath=None, interpolate_PTM=False, debug=False,
+            assets_dir="assets"):
+    """analysis.compute (analysis.py:414-482) for stored frames: read the frames dataset,
+    run steps 2-4 on the GPU and write the relight tables the reference's
+    interactive_relighting.compute() loads.  Video sync / frame extraction and the e-mail
+    notification are host-side features out of scope."""
+    from . import io as rio
+
+    if not from_storage:
+        raise NotImplementedError("frame extraction from video stays on the host (out of scope)")
+    frames_path = storage_filepath or os.path.join(assets_dir, f"frames_results_{video_name}")
+    results_frames = rio.read_from_file(frames_path)
+    tables = compute_tables(results_frames, interpolate_PTM=interpolate_PTM, first_only=debug)
+    if not debug:
+        rio.write_tables(tables, os.path.join(assets_dir, f"interpolation_results_{video_name}"))
+    return tables

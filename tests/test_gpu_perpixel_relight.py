@@ -176,3 +176,25 @@ def test_relight_tables_and_lookup(cuda):
     lxy = o.draw_light_roi_position(200, 100, (400, 400), to_light_vector=True)
     L = o.relight(d["coef"][:r, :r], "ptm", lxy[0], lxy[1]).reshape(r, r)
     assert np.array_equal(u8, np.clip(np.trunc(L), 0, 255).astype(np.uint8))
+
+
+@pytest.mark.parametrize("ptm", [True, False])
+def test_compat_compute_end_to_end(cuda, tmp_path, ptm):
+    """analysis.compute(from_storage=True) steps 2-4: frames .pbz2 -> GPU -> tables .pickle."""
+    from rti import io as rio
+
+    d = golden("ptm_perpixel_32x32_N50.npz")
+    data = [(d["frames"][i][:4, :4].copy(), d["cams"][i]) for i in range(len(d["cams"]))]
+    rio.write_on_file(data, str(tmp_path / "frames_results_coin9"))
+    tables = compat.compute("coin9", from_storage=True, interpolate_PTM=ptm, assets_dir=str(tmp_path))
+    assert tables.shape == (100, 100, 4, 4) and tables.dtype == np.int32
+    back = rio.read_tables(str(tmp_path / "interpolation_results_coin9"))
+    assert np.array_equal(back, tables)
+    if ptm:
+        ref_grid = d["grid"]  # the reference's own PTM grids for these 4x4 pixels
+        ref_t = d["tables"]
+    else:
+        r = golden("rbf_perpixel_4x4_N50.npz")
+        ref_grid, ref_t = r["grid"], r["tables"]
+    near = np.abs(ref_grid - np.round(ref_grid)) < 1e-4
+    assert not ((tables != ref_t) & ~np.transpose(near, (2, 3, 0, 1))).any()
