@@ -7,8 +7,9 @@
 // (LAPACK gesv: LU with partial pivoting) and evaluates f(q) = Σ_j w_j ‖q − x_j‖
 // on the 100×100 grid.  Every pixel has its own light list (compute_intensities,
 // analysis.py:225-231), so there is no shared operator: one workgroup owns one
-// pixel, factors its N×N system in LDS in fp64 (the systems reach cond ≈ 1e4–1e5
-// at N = 100–200) and streams the E evaluations, one query per lane.
+// pixel, factors its N×N system in LDS (fp32 factors + fp64 iterative refinement:
+// the systems reach cond ≈ 1e4–1e5 at N = 100–200) and streams the E evaluations,
+// one query per lane, in fp64.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -21,113 +22,294 @@ namespace rti {
 namespace {
 
 constexpr int RBF_MAX_N = 128;
+#ifndef RBF_MAX_REFINE
+#define RBF_MAX_REFINE 10  // refinement sweeps (tools/ builds probe variants with fewer)
+#endif
 
 template <typename T>
 __device__ __forceinline__ double ldd(const T* p) {
   return (double)*p;
 }
 
+// fp64 Euclidean distance between nodes i and j (pdist / cdist 'euclidean').
+__device__ __forceinline__ double dist64(double xi, double yi, double xj, double yj) {
+  const double dx = xi - xj, dy = yi - yj;
+  return sqrt(dx * dx + dy * dy);
+}
+
+// ‖·‖ for the evaluation sweep: fp32 rsqrt seed (≤ 2 ulp, 2⁻²² relative) and one fp64
+// Newton step, d = s·r + (s − (s·r)²)·r/2, relative error ≲ 2⁻⁴⁴ (≈ 6e-14) — 9 issue slots
+// against ≈ 17 for the correctly rounded fp64 sqrt.  With |Σ w_j d_j| terms ≲ 1e5 the
+// interpolated value moves by ≲ 1e-8 absolute.  The solve itself (A and the refinement
+// residuals) keeps the correctly rounded sqrt.
+__device__ __forceinline__ double dist_eval(double qu, double qv, double xj, double yj) {
+  const double dx = qu - xj, dy = qv - yj;
+  const double s = fma(dy, dy, dx * dx);
+#ifdef RBF_EXACT_EVAL
+  return sqrt(s);
+#else
+  const double r = (double)__builtin_amdgcn_rsqf(fmaxf((float)s, 1e-30f));
+  const double d0 = s * r;
+  return fma(fma(-d0, d0, s), 0.5 * r, d0);
+#endif
+}
+
+#ifdef RBF_TIMING  // probe builds only (tools/build_rbf_variants.sh): per-phase clocks of 256 blocks
+__device__ long long g_rbf_stamps[256][8];
+#define RBF_STAMP(i) \
+  if (tid == 0 && blockIdx.x < 256) g_rbf_stamps[blockIdx.x][i] = wall_clock64()
+#else
+#define RBF_STAMP(i)
+#endif
+
+__device__ __forceinline__ double readlane64(double x, int l) {
+  const uint64_t u = __double_as_longlong(x);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+
+// Per-lane view of the fp32 factors for wave 0's triangular solves.  The factorization
+// never moves rows: physical row i became the pivot of step so[i]; A[i][k] holds the
+// multiplier l_ik for k < so[i] and the U entry u_{so[i],k} for k ≥ so[i].  Lane l owns
+// physical rows l and l + 64 (N ≤ 128); the pivot list and the reciprocal diagonal are
+// lane-distributed by step and broadcast with readlane.
+struct LuLane {
+  int r0, r1;    // physical rows (clamped to N − 1 for the address when absent)
+  int s0, s1;    // their pivot steps (N when the row does not exist)
+  int pk0, pk1;  // piv[lane], piv[lane + 64]
+  double rd0, rd1;  // 1 / u_kk for k = lane, lane + 64
+};
+
+// z = U⁻¹ L⁻¹ P v on (v0, v1) = v at physical rows (lane, lane + 64); on return the
+// value held for physical row i is z at node so[i].  Column-oriented, one wave, the
+// chain runs through registers (readlane) and only the factor columns come from LDS.
+__device__ __forceinline__ void lu_solve_regs(const float* A, int lda, int N, const LuLane& q, double& v0,
+                                              double& v1, int lane) {
+  float c0 = A[q.r0 * lda], c1 = A[q.r1 * lda];
+  for (int k = 0; k < N; ++k) {  // forward: rows not yet pivoted at step k lose l_ik · y_k
+    const float n0 = A[q.r0 * lda + min(k + 1, N - 1)], n1 = A[q.r1 * lda + min(k + 1, N - 1)];
+    const int p = __builtin_amdgcn_readlane(k < 64 ? q.pk0 : q.pk1, k & 63);
+    const double y = readlane64(p < 64 ? v0 : v1, p & 63);
+    if (q.s0 > k) v0 = fma(-(double)c0, y, v0);
+    if (q.s1 > k) v1 = fma(-(double)c1, y, v1);
+    c0 = n0, c1 = n1;
+  }
+  c0 = A[q.r0 * lda + N - 1], c1 = A[q.r1 * lda + N - 1];
+  for (int k = N - 1; k >= 0; --k) {  // backward: z_k = y_k / u_kk; earlier pivots lose u_ik · z_k
+    const float n0 = A[q.r0 * lda + max(k - 1, 0)], n1 = A[q.r1 * lda + max(k - 1, 0)];
+    const int p = __builtin_amdgcn_readlane(k < 64 ? q.pk0 : q.pk1, k & 63);
+    const double z = readlane64(p < 64 ? v0 : v1, p & 63) * readlane64(k < 64 ? q.rd0 : q.rd1, k & 63);
+    if (q.s0 == k) v0 = z;
+    if (q.s1 == k) v1 = z;
+    if (q.s0 < k) v0 = fma(-(double)c0, z, v0);
+    if (q.s1 < k) v1 = fma(-(double)c1, z, v1);
+    c0 = n0, c1 = n1;
+  }
+}
+
+// One workgroup (4 waves) per pixel.  The distance matrix is factored in fp32 in LDS
+// (LU with partial pivoting; 40 KB at N = 100, so several pixels share a CU) and the
+// solution is brought to fp64 accuracy by mixed-precision iterative refinement: the
+// residual b − A·w is formed in fp64 from the node coordinates (A is never stored in
+// fp64) and the correction solved with the fp32 factors.  Each sweep shrinks the error
+// by ≈cond(A)·2⁻²⁴ (≤ 6e-3 up to cond 1e5); sweeps stop when the correction stops
+// shrinking or falls below 1e-16 of the solution.
+//
+// Elimination: rows are never swapped.  Wave w owns physical rows i ≡ w (mod 4) and
+// keeps the not-yet-pivoted ones in a bit mask; lanes own columns.  Step k updates the
+// wave's remaining rows against pivot row p and, in the same pass, lane 0 (column k+1)
+// tracks the largest |a_i,k+1| — the next pivot candidate — so a step costs one barrier.
 template <typename T, typename TO, int OL>
 __global__ void __launch_bounds__(256)
 rbf_perpixel(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
              const double* __restrict__ luv, int E, TO* __restrict__ out, int* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int lda = N + 1;  // odd row pitch: column walks do not hit one bank
-  double* A = smem;                       // [N][lda]
-  double* xs = A + (size_t)N * lda;       // [N]
-  double* ys = xs + N;                    // [N]
-  double* d = ys + N;                     // [N] right-hand side, then the solution w
-  __shared__ int s_piv;
-  __shared__ int s_sing;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lda = (N + 2) & ~1;  // even row pitch (floats) with ≥ 1 zero pad column: 8-byte pairs
+  double* xs = smem;      // [N] node coordinates (fp64 copies of the fp32 light vectors)
+  double* ys = xs + N;    // [N]
+  double* b = ys + N;     // [N] intensities (the right-hand side)
+  double* w = b + N;      // [N] solution, by node
+  double* v = w + N;      // [N] residual, by physical row
+  int* piv = reinterpret_cast<int*>(v + N);  // [N] pivot row of each step
+  int* so = piv + N;                         // [N] pivot step of each row
+  float* A = reinterpret_cast<float*>(so + N);  // [N][lda] fp32 LU factors
+  __shared__ float s_pmax[2][4];
+  __shared__ int s_pidx[2][4];
+  __shared__ int s_more;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: row ownership, masks, branches
   const int64_t p = blockIdx.x;
   const int64_t base = p * N;
+  RBF_STAMP(5);
 
   for (int j = tid; j < N; j += 256) {
     xs[j] = (double)lu[base + j];  // SciPy holds float64 copies of the float32 nodes
     ys[j] = (double)lv[base + j];
-    d[j] = ldd(I + base + j);
+    b[j] = ldd(I + base + j);
   }
-  if (tid == 0) s_sing = 0;
   __syncthreads();
-  for (int idx = tid; idx < N * N; idx += 256) {
-    const int i = idx / N, j = idx - i * N;
-    const double dx = xs[i] - xs[j], dy = ys[i] - ys[j];
-    A[i * lda + j] = sqrt(dx * dx + dy * dy);
+  for (int idx = tid; idx < N * lda; idx += 256) {
+    const int i = idx / lda, j = idx - i * lda;
+    A[idx] = j < N ? (float)dist64(xs[i], ys[i], xs[j], ys[j]) : 0.f;
   }
   __syncthreads();
 
-  // ---- LU with partial pivoting; the row operations are applied to d on the fly ----
-  for (int k = 0; k < N; ++k) {
-    if (wave == 0) {  // pivot: first row with the largest |A[i][k]|, i >= k (idamax)
-      double best = -1.0;
-      int bi = N;
-      for (int i = k + lane; i < N; i += 64) {
-        const double v = fabs(A[i * lda + k]);
-        if (v > best) best = v, bi = i;
-      }
+  RBF_STAMP(0);
+  uint32_t mask = 0;  // this wave's rows that are not pivots yet (bit s ↔ row wave + 4s)
+  {
+    const int i = wave + 4 * lane;
+    float best = -1.f;
+    int bi = N;
+    if (lane < 32 && i < N) best = fabsf(A[i * lda]), bi = i;
+    mask = __builtin_amdgcn_readfirstlane((uint32_t)__ballot(lane < 32 && i < N));
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const double ob = __shfl_xor(best, off);
-        const int oi = __shfl_xor(bi, off);
-        if (ob > best || (ob == best && oi < bi)) best = ob, bi = oi;
-      }
-      if (lane == 0) {
-        s_piv = bi;
-        if (!(best > 0.0)) s_sing = 1;
+    for (int off = 32; off > 0; off >>= 1) {
+      const float ob = __shfl_xor(best, off);
+      const int oi = __shfl_xor(bi, off);
+      if (ob > best || (ob == best && oi < bi)) best = ob, bi = oi;
+    }
+    if (lane == 0) s_pmax[0][wave] = best, s_pidx[0][wave] = bi;
+  }
+
+  bool singular = false;
+#ifndef RBF_PROBE_NO_LU
+  for (int k = 0; k < N; ++k) {
+#else
+  for (int k = 0; k < 0; ++k) {
+#endif
+    __syncthreads();
+    float best = s_pmax[k & 1][0];
+    int pr = s_pidx[k & 1][0];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float ob = s_pmax[k & 1][q];
+      const int oi = s_pidx[k & 1][q];
+      if (ob > best || (ob == best && oi < pr)) best = ob, pr = oi;
+    }
+    pr = __builtin_amdgcn_readfirstlane(pr);  // identical on every lane
+    if (!(best > 0.f)) {  // block-uniform: an exactly zero pivot column
+      singular = true;
+      break;
+    }
+    if (tid == 0) piv[k] = pr, so[pr] = k;
+    if ((pr & 3) == wave) mask &= ~(1u << (pr >> 2));
+    const float inv = 1.f / A[pr * lda + k];
+    // lane l owns the column pair (kb + 2l, kb + 2l + 1), kb = k rounded down to even:
+    // one 8-byte LDS access per row.  Pivot entries at columns ≤ k are zeroed so those
+    // columns pass through unchanged, and column k receives the multiplier l_ik.
+    const int kb = k & ~1, c0 = kb + 2 * lane;
+    const bool kodd = k & 1;
+    float bm = -1.f;
+    int bidx = N;
+    if (c0 < N) {
+      float2 pp = *reinterpret_cast<const float2*>(A + pr * lda + c0);
+      if (c0 <= k) pp.x = 0.f;
+      if (c0 + 1 <= k) pp.y = 0.f;
+      const bool put0 = lane == 0 && !kodd, put1 = lane == 0 && kodd;
+      // rows in batches of RB: all LDS reads of a batch are issued before its first use
+      constexpr int RB = 8;
+      for (uint32_t m = mask; m;) {
+        int ri[RB];
+        float lk[RB];
+        float2 av[RB];
+#pragma unroll
+        for (int t = 0; t < RB; ++t) {
+          ri[t] = m ? wave + 4 * __builtin_ctz(m) : -1;
+          m &= m - 1;
+        }
+#pragma unroll
+        for (int t = 0; t < RB; ++t)
+          if (ri[t] >= 0) {
+            const float* row = A + ri[t] * lda;
+            lk[t] = row[k];
+            av[t] = *reinterpret_cast<const float2*>(row + c0);
+          }
+#pragma unroll
+        for (int t = 0; t < RB; ++t)
+          if (ri[t] >= 0) {
+            const float l = lk[t] * inv;
+            float2 n;
+            n.x = put0 ? l : fmaf(-l, pp.x, av[t].x);
+            n.y = put1 ? l : fmaf(-l, pp.y, av[t].y);
+            *reinterpret_cast<float2*>(A + ri[t] * lda + c0) = n;
+            const float tv = fabsf(kodd ? n.x : n.y);  // column k + 1 on lane (k & 1)
+            if (tv > bm) bm = tv, bidx = ri[t];
+          }
       }
     }
-    __syncthreads();
-    const int pv = s_piv;
-    if (s_sing) break;  // uniform across the workgroup
-    if (pv != k) {
-      for (int j = k + tid; j < N; j += 256) {
-        const double t = A[k * lda + j];
-        A[k * lda + j] = A[pv * lda + j];
-        A[pv * lda + j] = t;
-      }
-      if (tid == 0) {
-        const double t = d[k];
-        d[k] = d[pv];
-        d[pv] = t;
+    if (lane == (k & 1)) s_pmax[(k + 1) & 1][wave] = bm, s_pidx[(k + 1) & 1][wave] = bidx;
+  }
+  RBF_STAMP(1);
+  if (singular && tid == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
+  __syncthreads();
+
+  if (!singular) {
+    LuLane q;
+    double v0 = 0.0, v1 = 0.0;
+    if (wave == 0) {
+      q.r0 = min(lane, N - 1), q.r1 = min(lane + 64, N - 1);
+      q.s0 = lane < N ? so[lane] : N, q.s1 = lane + 64 < N ? so[lane + 64] : N;
+      q.pk0 = piv[min(lane, N - 1)], q.pk1 = piv[min(lane + 64, N - 1)];
+      q.rd0 = 1.0 / (double)A[q.pk0 * lda + min(lane, N - 1)];
+      q.rd1 = 1.0 / (double)A[q.pk1 * lda + min(lane + 64, N - 1)];
+      v0 = lane < N ? b[lane] : 0.0, v1 = lane + 64 < N ? b[lane + 64] : 0.0;
+      lu_solve_regs(A, lda, N, q, v0, v1, lane);
+      if (lane < N) w[q.s0] = v0;
+      if (lane + 64 < N) w[q.s1] = v1;
+    }
+    RBF_STAMP(2);
+    double dprev = __builtin_inf();
+    for (int it = 0; it < RBF_MAX_REFINE; ++it) {
+      __syncthreads();
+      // v = b − A w in fp64, two threads per row (A recomputed from the coordinates)
+      {
+        const int i = tid >> 1, h = tid & 1;
+        double r = 0.0;
+        if (i < N) {
+          const double xi = xs[i], yi = ys[i];
+          for (int j = h; j < N; j += 2) r = fma(-dist64(xi, yi, xs[j], ys[j]), w[j], r);
+        }
+        r += __shfl_xor(r, 1);
+        if (i < N && h == 0) v[i] = b[i] + r;
       }
       __syncthreads();
-    }
-    const double inv = 1.0 / A[k * lda + k];
-    for (int i = k + 1 + tid; i < N; i += 256) A[i * lda + k] *= inv;  // multipliers l_i
-    __syncthreads();
-    const int m = N - k - 1;
-    const double dk = d[k];
-    for (int idx = tid; idx < m * (m + 1); idx += 256) {  // trailing update, plus column N = rhs
-      const int ii = idx / (m + 1), jj = idx - ii * (m + 1);
-      const int i = k + 1 + ii;
-      const double l = A[i * lda + k];
-      if (jj < m) {
-        const int j = k + 1 + jj;
-        A[i * lda + j] = fma(-l, A[k * lda + j], A[i * lda + j]);
-      } else {
-        d[i] = fma(-l, dk, d[i]);
+      if (wave == 0) {
+        v0 = lane < N ? v[lane] : 0.0, v1 = lane + 64 < N ? v[lane + 64] : 0.0;
+        lu_solve_regs(A, lda, N, q, v0, v1, lane);
+        double dn = 0.0, wn = 0.0;
+        if (lane < N) {
+          const double t = w[q.s0] + v0;
+          w[q.s0] = t;
+          dn = fabs(v0), wn = fabs(t);
+        }
+        if (lane + 64 < N) {
+          const double t = w[q.s1] + v1;
+          w[q.s1] = t;
+          dn = fmax(dn, fabs(v1)), wn = fmax(wn, fabs(t));
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          dn = fmax(dn, __shfl_xor(dn, off));
+          wn = fmax(wn, __shfl_xor(wn, off));
+        }
+        // remaining error ≈ ρ·dn with ρ = dn / dprev the observed contraction; stop at the
+        // fp64 floor (≈ cond·eps) or when a sweep no longer halves the correction
+        if (lane == 0)
+          s_more = dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
+        dprev = dn;
       }
-    }
-    __syncthreads();
-  }
-  const bool singular = s_sing != 0;
-  if (singular && tid == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
-
-  // ---- back substitution U w = d, one wave (lock-step; LDS ordered within the wave) ----
-  if (!singular && wave == 0) {
-    for (int i = N - 1; i >= 0; --i) {
-      const double wi = d[i] / A[i * lda + i];
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) d[i] = wi;
-      for (int j = lane; j < i; j += 64) d[j] = fma(-A[j * lda + i], wi, d[j]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __syncthreads();
+      if (!s_more) {
+#ifdef RBF_TIMING
+        if (tid == 0 && blockIdx.x < 256) g_rbf_stamps[blockIdx.x][7] = it + 1;
+#endif
+        break;  // uniform
+      }
     }
   }
   __syncthreads();
 
+  RBF_STAMP(3);
   // ---- evaluate f(q_e) = Σ_j w_j ‖q_e − x_j‖ (cdist · nodes, analysis.py:260) ----
   for (int e = tid; e < E; e += 256) {
     double f;
@@ -136,22 +318,23 @@ rbf_perpixel(const float* __restrict__ lu, const float* __restrict__ lv, const T
     } else {
       const double qu = luv[2 * e], qv = luv[2 * e + 1];
       f = 0.0;
-      for (int j = 0; j < N; ++j) {
-        const double dx = qu - xs[j], dy = qv - ys[j];
-        f = fma(d[j], sqrt(dx * dx + dy * dy), f);
-      }
+      for (int j = 0; j < N; ++j) f = fma(w[j], dist_eval(qu, qv, xs[j], ys[j]), f);
     }
     if constexpr (OL == RTI_OUT_PIXEL_MAJOR)
       out[p * E + e] = cvt_out<TO>(f);
     else
       out[(int64_t)e * P + p] = cvt_out<TO>(f);
   }
+#ifdef RBF_TIMING
+  __syncthreads();
+#endif
+  RBF_STAMP(4);
 }
 
 template <typename T, typename TO>
 void launch_ol(int ol, const float* lu, const float* lv, const void* I, int N, int64_t P, const double* luv, int E,
                void* out, int* status, hipStream_t s) {
-  const size_t lds = ((size_t)N * (N + 1) + 3 * (size_t)N) * sizeof(double);
+  const size_t lds = 5 * (size_t)N * sizeof(double) + 2 * (size_t)N * sizeof(int) + (size_t)N * ((N + 2) & ~1) * sizeof(float);
   if (lds > 65536) {  // opt in to more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rbf_perpixel<T, TO, RTI_OUT_PIXEL_MAJOR>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -181,6 +364,12 @@ void launch_out(int odt, int ol, const float* lu, const float* lv, const void* I
 }  // namespace rti
 
 using namespace rti;
+
+#ifdef RBF_TIMING
+extern "C" int rti_rbf_probe_stamps(long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(rti::g_rbf_stamps), sizeof(rti::g_rbf_stamps)) == hipSuccess ? 0 : 3;
+}
+#endif
 
 extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                                 const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
