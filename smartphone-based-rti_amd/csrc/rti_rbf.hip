@@ -42,9 +42,7 @@ __device__ __forceinline__ double dist64(double xi, double yi, double xj, double
 // against ≈ 17 for the correctly rounded fp64 sqrt.  With |Σ w_j d_j| terms ≲ 1e5 the
 // interpolated value moves by ≲ 1e-8 absolute.  The solve itself (A and the refinement
 // residuals) keeps the correctly rounded sqrt.
-__device__ __forceinline__ double dist_eval(double qu, double qv, double xj, double yj) {
-  const double dx = qu - xj, dy = qv - yj;
-  const double s = fma(dy, dy, dx * dx);
+__device__ __forceinline__ double norm_eval(double s) {
 #ifdef RBF_EXACT_EVAL
   return sqrt(s);
 #else
@@ -52,6 +50,11 @@ __device__ __forceinline__ double dist_eval(double qu, double qv, double xj, dou
   const double d0 = s * r;
   return fma(fma(-d0, d0, s), 0.5 * r, d0);
 #endif
+}
+
+__device__ __forceinline__ double dist_eval(double qu, double qv, double xj, double yj) {
+  const double dx = qu - xj, dy = qv - yj;
+  return norm_eval(fma(dy, dy, dx * dx));
 }
 
 #ifdef RBF_TIMING  // probe builds only (tools/build_rbf_variants.sh): per-phase clocks of 256 blocks
@@ -107,6 +110,7 @@ __device__ __forceinline__ void lu_solve_regs(const float* A, int lda, int N, co
   }
 }
 
+// Fallback for 112 < N ≤ 128 (register budget of rbf_solve_gj).
 // One workgroup (4 waves) per pixel.  The distance matrix is factored in fp32 in LDS
 // (LU with partial pivoting; 40 KB at N = 100, so several pixels share a CU) and the
 // solution is brought to fp64 accuracy by mixed-precision iterative refinement: the
@@ -119,10 +123,10 @@ __device__ __forceinline__ void lu_solve_regs(const float* A, int lda, int N, co
 // keeps the not-yet-pivoted ones in a bit mask; lanes own columns.  Step k updates the
 // wave's remaining rows against pivot row p and, in the same pass, lane 0 (column k+1)
 // tracks the largest |a_i,k+1| — the next pivot candidate — so a step costs one barrier.
-template <typename T, typename TO, int OL>
+template <typename T>
 __global__ void __launch_bounds__(256)
-rbf_perpixel(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
-             const double* __restrict__ luv, int E, TO* __restrict__ out, int* __restrict__ status) {
+rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
+              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int lda = (N + 2) & ~1;  // even row pitch (floats) with ≥ 1 zero pad column: 8-byte pairs
   double* xs = smem;      // [N] node coordinates (fp64 copies of the fp32 light vectors)
@@ -310,54 +314,227 @@ rbf_perpixel(const float* __restrict__ lu, const float* __restrict__ lv, const T
   __syncthreads();
 
   RBF_STAMP(3);
-  // ---- evaluate f(q_e) = Σ_j w_j ‖q_e − x_j‖ (cdist · nodes, analysis.py:260) ----
-  for (int e = tid; e < E; e += 256) {
-    double f;
-    if (singular) {
-      f = __builtin_nan("");
-    } else {
-      const double qu = luv[2 * e], qv = luv[2 * e + 1];
-      f = 0.0;
-      for (int j = 0; j < N; ++j) f = fma(w[j], dist_eval(qu, qv, xs[j], ys[j]), f);
-    }
-    if constexpr (OL == RTI_OUT_PIXEL_MAJOR)
-      out[p * E + e] = cvt_out<TO>(f);
-    else
-      out[(int64_t)e * P + p] = cvt_out<TO>(f);
+  for (int j = tid; j < N; j += 256) {
+    wT[(int64_t)j * P + p] = singular ? __builtin_nan("") : w[j];
+    xyT[(int64_t)j * P + p] = make_float2(lu[base + j], lv[base + j]);
   }
-#ifdef RBF_TIMING
-  __syncthreads();
-#endif
-  RBF_STAMP(4);
 }
 
-template <typename T, typename TO>
-void launch_ol(int ol, const float* lu, const float* lv, const void* I, int N, int64_t P, const double* luv, int E,
-               void* out, int* status, hipStream_t s) {
-  const size_t lds = 5 * (size_t)N * sizeof(double) + 2 * (size_t)N * sizeof(int) + (size_t)N * ((N + 2) & ~1) * sizeof(float);
-  if (lds > 65536) {  // opt in to more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rbf_perpixel<T, TO, RTI_OUT_PIXEL_MAJOR>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rbf_perpixel<T, TO, RTI_OUT_EVAL_MAJOR>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  }
-  if (ol == RTI_OUT_PIXEL_MAJOR)
-    hipLaunchKernelGGL((rbf_perpixel<T, TO, RTI_OUT_PIXEL_MAJOR>), dim3((unsigned)P), dim3(256), lds, s, lu, lv,
-                       static_cast<const T*>(I), N, P, luv, E, static_cast<TO*>(out), status);
-  else
-    hipLaunchKernelGGL((rbf_perpixel<T, TO, RTI_OUT_EVAL_MAJOR>), dim3((unsigned)P), dim3(256), lds, s, lu, lv,
-                       static_cast<const T*>(I), N, P, luv, E, static_cast<TO*>(out), status);
+// Wave-wide max of a u32 key: DPP within each row of 16 lanes, then the four row maxima
+// through readlane (scalar).  No LDS round trips on the pivot search's critical path.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+  const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+  const uint32_t r2 = __builtin_amdgcn_readlane(v, 47), r3 = __builtin_amdgcn_readlane(v, 63);
+  return max(max(r0, r1), max(r2, r3));
 }
+
+// Per-pixel solve for N ≤ NMAX ≤ 112: Gauss-Jordan elimination with partial pivoting in
+// fp64 registers (what SciPy's gesv computes, to rounding: cond·eps ≈ 1e-12 relative).
+//
+// One workgroup per pixel, one thread per row: thread t holds row t of [A | b] in
+// registers, a[0..NMAX) fp64.  After step k every row shifts left by one, so the column
+// being eliminated is always a[0] and every register index is a compile-time constant;
+// the live width N − k shrinks, and the step body is instantiated for widths NMAX,
+// NMAX − 8, …, 8 (phases) so the work follows the triangle.  Gauss-Jordan also
+// eliminates above the pivot — free here, since every row is updated in lock-step anyway
+// — which leaves the system diagonal: x at node k is b[p_k] / pivot_k, with no L or U
+// storage and no substitution passes.
+//
+// Pivot search: key = (float bits of |a_t0| with the low 7 bits replaced by 127 − t),
+// reduced across the wave with DPP; ties and near-ties (2⁻¹⁶ relative) go to the lower
+// row.  Each wave stages its candidate row in LDS, one barrier, and every thread reads
+// the winner's row with broadcast loads.
+template <int NMAX, typename T>
+struct GjSolve {
+  static constexpr int WAVES = NMAX <= 64 ? 1 : 2;
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int LDR = NMAX + 2;  // staged row: a[1..], b at [NMAX], 16-byte aligned pitch
+
+  struct Smem {
+    double xs[NMAX], ys[NMAX];
+    __attribute__((aligned(16))) double stage[2][WAVES][LDR];
+    uint32_t key[2][WAVES];
+  };
+
+  // One elimination step at static width WS (N − k ≤ WS).
+  template <int WS>
+  static __device__ __forceinline__ bool step(Smem& sm, double (&a)[NMAX], double& b, bool& used, int& my_step,
+                                              double& my_d, int k, int t, int wave) {
+    uint32_t key = 0;
+    if (!used) key = (__float_as_uint((float)fabs(a[0])) & ~127u) | (uint32_t)(127 - t);
+    key = wave_max_u32(key);
+    const int buf = k & 1;
+    if (t == 127 - (int)(key & 127u) && (key >> 7)) {  // this wave's candidate row → LDS
+      double* r = sm.stage[buf][wave];
+#pragma unroll
+      for (int s = 1; s < WS; ++s) r[s - 1] = a[s];
+      r[NMAX] = b;
+      r[NMAX + 1] = a[0];
+    }
+    if ((t & 63) == 0) sm.key[buf][wave] = key;
+    __syncthreads();
+    uint32_t best = sm.key[buf][0];
+    int win = 0;
+    if constexpr (WAVES == 2) {
+      const uint32_t k1 = sm.key[buf][1];
+      if (k1 > best) best = k1, win = 1;
+    }
+    if (!(best >> 7)) return false;  // exactly zero pivot column: singular
+    const int pr = 127 - (int)(best & 127u);
+    const double* r = sm.stage[buf][win];
+    const double piv = r[NMAX + 1];
+    const bool me = t == pr;
+    const double l = me ? 0.0 : a[0] * (1.0 / piv);
+    if (me) used = true, my_step = k, my_d = piv;
+#pragma unroll
+    for (int s = 1; s < WS; ++s) a[s - 1] = fma(-l, r[s - 1], a[s]);
+    b = fma(-l, r[NMAX], b);
+    return true;
+  }
+
+  template <int WS>
+  static __device__ __forceinline__ bool phases(Smem& sm, double (&a)[NMAX], double& b, bool& used, int& my_step,
+                                                double& my_d, int& k, int N, int t, int wave) {
+    for (; k < N && N - k > WS - 8; ++k)
+      if (!step<WS>(sm, a, b, used, my_step, my_d, k, t, wave)) return false;
+    if constexpr (WS > 8) return phases<WS - 8>(sm, a, b, used, my_step, my_d, k, N, t, wave);
+    return true;
+  }
+};
+
+template <int NMAX, typename T>
+__global__ void __launch_bounds__(NMAX <= 64 ? 64 : 128)
+rbf_solve_gj(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
+             double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status) {
+  using G = GjSolve<NMAX, T>;
+  __shared__ typename G::Smem sm;
+  const int t = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t p = blockIdx.x;
+  const int64_t base = p * N;
+  if (t < N) {
+    const float x = lu[base + t], y = lv[base + t];
+    sm.xs[t] = (double)x;  // SciPy holds float64 copies of the float32 nodes
+    sm.ys[t] = (double)y;
+    xyT[(int64_t)t * P + p] = make_float2(x, y);
+  }
+  double b = t < N ? ldd(I + base + t) : 0.0;
+  __syncthreads();
+  double a[NMAX];
+  {
+    const int tc = min(t, N - 1);
+    const double xi = sm.xs[tc], yi = sm.ys[tc];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) a[j] = (j < N && t < N) ? dist64(xi, yi, sm.xs[min(j, N - 1)], sm.ys[min(j, N - 1)]) : 0.0;
+  }
+  bool used = t >= N;  // rows past N: zero, never pivots, never read
+  int my_step = 0;
+  double my_d = 1.0;
+  int k = 0;
+  const bool ok = G::template phases<NMAX>(sm, a, b, used, my_step, my_d, k, N, t, wave);
+  if (!ok && t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
+  if (t < N) wT[(int64_t)(ok ? my_step : t) * P + p] = ok ? b / my_d : __builtin_nan("");
+}
+
+// f(q_e) = Σ_j w_j ‖q_e − x_j‖ for a 64-pixel tile × 4·TE queries per workgroup (TE = 20:
+// a wave's queries then lie in one row of the reference's 100 × 100 grid and share (qv − y)²).  Lanes
+// run over pixels (node tables are [N][P], so each load is one coalesced 512-byte row and
+// eval-major stores are coalesced); each thread keeps TE accumulators, the queries are
+// wave-uniform (scalar loads).  fp64 throughout; ‖·‖ via dist_eval.
+template <int TE, typename TO, int OL>
+__global__ void __launch_bounds__(256)
+rbf_eval(const double* __restrict__ wT, const float2* __restrict__ xyT, int N, int64_t P,
+         const double* __restrict__ luv, int E, TO* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int e0 = (blockIdx.x * 4 + wave) * TE;
+  if (e0 >= E) return;  // wave-uniform
+  const int64_t p = (int64_t)blockIdx.y * 64 + lane;
+  const int64_t pc = p < P ? p : P - 1;
+  double qu[TE], qv[TE], acc[TE];
+#pragma unroll
+  for (int i = 0; i < TE; ++i) {
+    const int e = min(e0 + i, E - 1);
+    qu[i] = luv[2 * e], qv[i] = luv[2 * e + 1], acc[i] = 0.0;
+  }
+  bool same_v = true;  // a grid row: every query of this wave shares qv, so (qv − y)² is shared
+#pragma unroll
+  for (int i = 1; i < TE; ++i) same_v = same_v && qv[i] == qv[0];
+  if (same_v) {
+    for (int j = 0; j < N; ++j) {
+      const double w = wT[(int64_t)j * P + pc];
+      const float2 xy = xyT[(int64_t)j * P + pc];
+      const double x = xy.x, dy = qv[0] - (double)xy.y, dy2 = dy * dy;
+#pragma unroll
+      for (int i = 0; i < TE; ++i) {
+        const double dx = qu[i] - x;
+        acc[i] = fma(w, norm_eval(fma(dx, dx, dy2)), acc[i]);
+      }
+    }
+  } else {
+    for (int j = 0; j < N; ++j) {
+      const double w = wT[(int64_t)j * P + pc];
+      const float2 xy = xyT[(int64_t)j * P + pc];
+      const double x = xy.x, y = xy.y;
+#pragma unroll
+      for (int i = 0; i < TE; ++i) acc[i] = fma(w, dist_eval(qu[i], qv[i], x, y), acc[i]);
+    }
+  }
+  if (p >= P) return;
+#pragma unroll
+  for (int i = 0; i < TE; ++i) {
+    const int e = e0 + i;
+    if (e < E) {
+      if constexpr (OL == RTI_OUT_PIXEL_MAJOR)
+        out[p * E + e] = cvt_out<TO>(acc[i]);
+      else
+        out[(int64_t)e * P + p] = cvt_out<TO>(acc[i]);
+    }
+  }
+}
+
+constexpr int RBF_GJ_MAX_N = 112;
+constexpr int RBF_TE = 20;  // divides the reference's 100-wide grid rows (shared qv)
 
 template <typename T>
-void launch_out(int odt, int ol, const float* lu, const float* lv, const void* I, int N, int64_t P, const double* luv,
-                int E, void* out, int* status, hipStream_t s) {
-  switch (odt) {
-    case RTI_F64: launch_ol<T, double>(ol, lu, lv, I, N, P, luv, E, out, status, s); break;
-    case RTI_F32: launch_ol<T, float>(ol, lu, lv, I, N, P, luv, E, out, status, s); break;
-    case RTI_I32: launch_ol<T, int32_t>(ol, lu, lv, I, N, P, luv, E, out, status, s); break;
-    default: launch_ol<T, uint8_t>(ol, lu, lv, I, N, P, luv, E, out, status, s); break;
+void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
+                  int* status, hipStream_t s) {
+  const T* In = static_cast<const T*>(I);
+  const dim3 g((unsigned)P);
+#define RBF_GJ(NM)                                                                                       \
+  hipLaunchKernelGGL((rbf_solve_gj<NM, T>), g, dim3(GjSolve<NM, T>::THREADS), 0, s, lu, lv, In, N, P, wT, \
+                     xyT, status)
+  if (N <= 16) RBF_GJ(16);
+  else if (N <= 32) RBF_GJ(32);
+  else if (N <= 48) RBF_GJ(48);
+  else if (N <= 64) RBF_GJ(64);
+  else if (N <= 80) RBF_GJ(80);
+  else if (N <= 96) RBF_GJ(96);
+  else if (N <= RBF_GJ_MAX_N) RBF_GJ(112);
+  else {
+    const size_t lds = 5 * (size_t)N * sizeof(double) + 2 * (size_t)N * sizeof(int) + (size_t)N * ((N + 2) & ~1) * sizeof(float);
+    if (lds > 65536)  // opt in to more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rbf_solve_lds<T>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((rbf_solve_lds<T>), g, dim3(256), lds, s, lu, lv, In, N, P, wT, xyT, status);
   }
+#undef RBF_GJ
+}
+
+template <typename TO>
+void launch_eval(int ol, const double* wT, const float2* xyT, int N, int64_t P, const double* luv, int E, void* out,
+                 hipStream_t s) {
+  const dim3 g((unsigned)((E + 4 * RBF_TE - 1) / (4 * RBF_TE)), (unsigned)((P + 63) / 64));
+  if (ol == RTI_OUT_PIXEL_MAJOR)
+    hipLaunchKernelGGL((rbf_eval<RBF_TE, TO, RTI_OUT_PIXEL_MAJOR>), g, dim3(256), 0, s, wT, xyT, N, P, luv, E,
+                       static_cast<TO*>(out));
+  else
+    hipLaunchKernelGGL((rbf_eval<RBF_TE, TO, RTI_OUT_EVAL_MAJOR>), g, dim3(256), 0, s, wT, xyT, N, P, luv, E,
+                       static_cast<TO*>(out));
 }
 
 }  // namespace
@@ -384,11 +561,28 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
     return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: out dtype %d", out_dtype);
   if (out_layout != RTI_OUT_PIXEL_MAJOR && out_layout != RTI_OUT_EVAL_MAJOR)
     return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: out layout %d", out_layout);
+  if ((int64_t)((E + 4 * RBF_TE - 1) / (4 * RBF_TE)) > 0x7fffffff || (P + 63) / 64 > 65535)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: grid too large (P=%lld, E=%d)", (long long)P, E);
   hipStream_t s = (hipStream_t)stream;
+  // workspace: per-pixel weights and nodes, node-major ([N][P]) for the coalesced evaluation
+  void* ws = nullptr;
+  if (hipMallocAsync(&ws, (size_t)N * P * (sizeof(double) + sizeof(float2)), s) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_rbf_perpixel: workspace allocation of %zu bytes failed",
+                (size_t)N * P * (sizeof(double) + sizeof(float2)));
+  double* wT = static_cast<double*>(ws);
+  float2* xyT = reinterpret_cast<float2*>(wT + (size_t)N * P);
   switch (in_dtype) {
-    case RTI_F32: launch_out<float>(out_dtype, out_layout, lu, lv, I, N, P, luv, E, out, status, s); break;
-    case RTI_I32: launch_out<int32_t>(out_dtype, out_layout, lu, lv, I, N, P, luv, E, out, status, s); break;
-    default: launch_out<uint8_t>(out_dtype, out_layout, lu, lv, I, N, P, luv, E, out, status, s); break;
+    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, s); break;
+    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, s); break;
+    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, s); break;
   }
-  return check_launch("rti_rbf_perpixel");
+  switch (out_dtype) {
+    case RTI_F64: launch_eval<double>(out_layout, wT, xyT, N, P, luv, E, out, s); break;
+    case RTI_F32: launch_eval<float>(out_layout, wT, xyT, N, P, luv, E, out, s); break;
+    case RTI_I32: launch_eval<int32_t>(out_layout, wT, xyT, N, P, luv, E, out, s); break;
+    default: launch_eval<uint8_t>(out_layout, wT, xyT, N, P, luv, E, out, s); break;
+  }
+  const int rc = check_launch("rti_rbf_perpixel");
+  (void)hipFreeAsync(ws, s);
+  return rc;
 }
