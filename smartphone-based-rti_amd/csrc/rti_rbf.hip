@@ -22,9 +22,7 @@ namespace rti {
 namespace {
 
 constexpr int RBF_MAX_N = 128;
-#ifndef RBF_MAX_REFINE
-#define RBF_MAX_REFINE 10  // refinement sweeps (tools/ builds probe variants with fewer)
-#endif
+constexpr int RBF_MAX_REFINE = 10;  // refinement sweeps of the fp32-LU fallback
 
 template <typename T>
 __device__ __forceinline__ double ldd(const T* p) {
@@ -43,13 +41,9 @@ __device__ __forceinline__ double dist64(double xi, double yi, double xj, double
 // interpolated value moves by ≲ 1e-8 absolute.  The solve itself (A and the refinement
 // residuals) keeps the correctly rounded sqrt.
 __device__ __forceinline__ double norm_eval(double s) {
-#ifdef RBF_EXACT_EVAL
-  return sqrt(s);
-#else
   const double r = (double)__builtin_amdgcn_rsqf(fmaxf((float)s, 1e-30f));
   const double d0 = s * r;
   return fma(fma(-d0, d0, s), 0.5 * r, d0);
-#endif
 }
 
 __device__ __forceinline__ double dist_eval(double qu, double qv, double xj, double yj) {
@@ -57,13 +51,6 @@ __device__ __forceinline__ double dist_eval(double qu, double qv, double xj, dou
   return norm_eval(fma(dy, dy, dx * dx));
 }
 
-#ifdef RBF_TIMING  // probe builds only (tools/build_rbf_variants.sh): per-phase clocks of 256 blocks
-__device__ long long g_rbf_stamps[256][8];
-#define RBF_STAMP(i) \
-  if (tid == 0 && blockIdx.x < 256) g_rbf_stamps[blockIdx.x][i] = wall_clock64()
-#else
-#define RBF_STAMP(i)
-#endif
 
 __device__ __forceinline__ double readlane64(double x, int l) {
   const uint64_t u = __double_as_longlong(x);
@@ -144,7 +131,6 @@ rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: row ownership, masks, branches
   const int64_t p = blockIdx.x;
   const int64_t base = p * N;
-  RBF_STAMP(5);
 
   for (int j = tid; j < N; j += 256) {
     xs[j] = (double)lu[base + j];  // SciPy holds float64 copies of the float32 nodes
@@ -158,7 +144,6 @@ rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const 
   }
   __syncthreads();
 
-  RBF_STAMP(0);
   uint32_t mask = 0;  // this wave's rows that are not pivots yet (bit s ↔ row wave + 4s)
   {
     const int i = wave + 4 * lane;
@@ -176,11 +161,7 @@ rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const 
   }
 
   bool singular = false;
-#ifndef RBF_PROBE_NO_LU
   for (int k = 0; k < N; ++k) {
-#else
-  for (int k = 0; k < 0; ++k) {
-#endif
     __syncthreads();
     float best = s_pmax[k & 1][0];
     int pr = s_pidx[k & 1][0];
@@ -243,7 +224,6 @@ rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const 
     }
     if (lane == (k & 1)) s_pmax[(k + 1) & 1][wave] = bm, s_pidx[(k + 1) & 1][wave] = bidx;
   }
-  RBF_STAMP(1);
   if (singular && tid == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
   __syncthreads();
 
@@ -261,7 +241,6 @@ rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const 
       if (lane < N) w[q.s0] = v0;
       if (lane + 64 < N) w[q.s1] = v1;
     }
-    RBF_STAMP(2);
     double dprev = __builtin_inf();
     for (int it = 0; it < RBF_MAX_REFINE; ++it) {
       __syncthreads();
@@ -303,17 +282,11 @@ rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const 
         dprev = dn;
       }
       __syncthreads();
-      if (!s_more) {
-#ifdef RBF_TIMING
-        if (tid == 0 && blockIdx.x < 256) g_rbf_stamps[blockIdx.x][7] = it + 1;
-#endif
-        break;  // uniform
-      }
+      if (!s_more) break;  // uniform
     }
   }
   __syncthreads();
 
-  RBF_STAMP(3);
   for (int j = tid; j < N; j += 256) {
     wT[(int64_t)j * P + p] = singular ? __builtin_nan("") : w[j];
     xyT[(int64_t)j * P + p] = make_float2(lu[base + j], lv[base + j]);
@@ -542,11 +515,6 @@ void launch_eval(int ol, const double* wT, const float2* xyT, int N, int64_t P, 
 
 using namespace rti;
 
-#ifdef RBF_TIMING
-extern "C" int rti_rbf_probe_stamps(long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(rti::g_rbf_stamps), sizeof(rti::g_rbf_stamps)) == hipSuccess ? 0 : 3;
-}
-#endif
 
 extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                                 const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
