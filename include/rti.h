@@ -194,6 +194,20 @@ int rti_relight(const void* coef, int coef_dtype, int basis, int64_t P, int coef
                 const double* luv, int E,
                 void* out, int out_dtype, int out_layout, rti_stream_t stream);
 
+/* ---- device: interactive relight frame ----------------------------------------------
+ * Replaces relighting_event's per-event image work (interactive_relighting.py:31-38):
+ * V = clip(value, 0, 255) (the in-place clip of :35-36), img[:, :, 2] = V (:37), then
+ * cv2.cvtColor(img, COLOR_HSV2BGR) (:38) for 8-bit images (OpenCV >= 4.2 HSV2RGB_b,
+ * hue range 180, restated in DESIGN.md §4.4).
+ *   src_dtype I32: src is the int32 table image [P] the cursor selected
+ *     (interpolation_results[int_ly][int_lx]); basis, coef_layout, lu, lv ignored.
+ *   src_dtype F32/F64: src is the coefficient map [P][k] / [k][P] (coef_layout) and
+ *     value = relight at (lu, lv) truncated to int32 exactly as rti_relight's I32 output.
+ * hsv: device uint8 [P][3] (the ROI in HSV, get_ROI(..., hsv=True)); bgr: device uint8
+ * [P][3] output, may not alias hsv. */
+int rti_relight_frame(const void* src, int src_dtype, int basis, int coef_layout, int64_t P,
+                      double lu, double lv, const uint8_t* hsv, uint8_t* bgr, rti_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

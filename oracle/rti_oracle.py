@@ -386,6 +386,48 @@ def relight_lookup(table, x, y, shape):
     return vals
 
 
+def hsv2bgr_u8(hsv):
+    """cv2.cvtColor(img, cv2.COLOR_HSV2BGR) for uint8 images, as called at
+    interactive_relighting.py:38 (OpenCV >= 4.2, README.md:46; OpenCV is not installed
+    here, so this restates its published HSV2RGB_b / HSV2RGB_native scalar algorithm,
+    hue range 180): s, v = S/255, V/255 and h = H·(6/180) in float32; sector = floor(h)
+    (h - 6 when h >= 6); tab = (v, v(1-s), v(1-s·f), v(1-s(1-f))); (b, g, r) by the
+    sector table {{1,3,0},{1,0,2},{3,0,1},{0,2,1},{0,1,3},{2,1,0}}; each channel
+    saturate_cast<uchar>(x·255) = round half to even, clamp.  s == 0 -> b = g = r = v.
+    Parity against OpenCV itself is unpinned; the known-answer tests pin the primaries."""
+    a = np.asarray(hsv, np.uint8)
+    f32 = np.float32
+    H = a[..., 0].astype(f32)
+    S = a[..., 1].astype(f32) * (f32(1.0) / f32(255.0))
+    V = a[..., 2].astype(f32) * (f32(1.0) / f32(255.0))
+    h = H * (f32(6.0) / f32(180.0))
+    h = np.where(h >= f32(6.0), h - f32(6.0), h).astype(f32)
+    sector = np.floor(h).astype(np.int32)
+    fr = (h - sector.astype(f32)).astype(f32)
+    bad = (sector < 0) | (sector >= 6)
+    sector = np.where(bad, 0, sector)
+    fr = np.where(bad, f32(0.0), fr).astype(f32)
+    one = f32(1.0)
+    tab = np.stack([V, V * (one - S), V * (one - S * fr), V * (one - S * (one - fr))], -1).astype(f32)
+    sd = np.array([[1, 3, 0], [1, 0, 2], [3, 0, 1], [0, 2, 1], [0, 1, 3], [2, 1, 0]])
+    idx = sd[sector]  # [..., 3]
+    bgr = np.take_along_axis(tab, idx, axis=-1)
+    bgr = np.where((S == 0)[..., None], V[..., None], bgr).astype(f32)
+    return np.clip(np.rint(bgr * f32(255.0)), 0, 255).astype(np.uint8)
+
+
+def relighting_event_image(values, roi_hsv):
+    """interactive_relighting.py:31-38 without the window: clip the selected int32 table
+    image in place semantics (values > 255 -> 255, values <= 0 -> 0), write it into the HSV
+    ROI's V channel and convert HSV -> BGR."""
+    v = np.array(values, copy=True)
+    v[v > 255] = 255
+    v[v <= 0] = 0
+    img = np.array(roi_hsv, np.uint8, copy=True)
+    img[:, :, 2] = v
+    return hsv2bgr_u8(img)
+
+
 # ----------------------------------------------------------------------------
 # Synthetic inputs (SURVEY §8(d) recipe)
 # ----------------------------------------------------------------------------

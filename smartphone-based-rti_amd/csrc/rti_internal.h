@@ -15,7 +15,7 @@ int fail(int status, const char* fmt, ...);
 // hipGetLastError after a launch -> RTI_OK or RTI_ERR_HIP.
 int check_launch(const char* what);
 
-inline bool aligned_to(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
+__host__ __device__ inline bool aligned_to(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
 inline unsigned grid_1d(int64_t items, int per_block) { return (unsigned)((items + per_block - 1) / per_block); }
 

@@ -174,6 +174,135 @@ void launch_k(const RelightArgs& a, int odt) {
   }
 }
 
+// ---- interactive relight frame (interactive_relighting.py:22-38) ---------------------
+// OpenCV 4.x COLOR_HSV2BGR for 8-bit images, hue range 180 (HSV2RGB_b + HSV2RGB_native,
+// scalar form): s and v scaled by 1/255 in fp32, h·(6/180), sector = floor, the four
+// tab[] products, saturate_cast<uchar>(x·255) = round-half-even then clamp.  No FP
+// contraction, so the oracle's NumPy restatement is matched bit for bit.
+__device__ __forceinline__ uint8_t sat_u8(float x) {
+  const float r = rintf(x);
+  return (uint8_t)(r < 0.f ? 0.f : (r > 255.f ? 255.f : r));
+}
+
+__device__ __forceinline__ void hsv2bgr_u8(uint32_t H, uint32_t S, uint32_t V, uint8_t (&bgr)[3]) {
+#pragma clang fp contract(off)
+  const float hscale = 6.0f / 180.0f;
+  const float s = (float)S * (1.0f / 255.0f);
+  const float v = (float)V * (1.0f / 255.0f);
+  float b, g, r;
+  if (s == 0.f) {
+    b = g = r = v;
+  } else {
+    float h = (float)H * hscale;
+    if (h >= 6.f) h -= 6.f;  // H <= 255 -> h < 8.5: one subtraction (OpenCV's loop / fmod)
+    int sector = (int)floorf(h);
+    h -= (float)sector;
+    if ((unsigned)sector >= 6u) {
+      sector = 0;
+      h = 0.f;
+    }
+    const float t0 = v, t1 = v * (1.f - s), t2 = v * (1.f - s * h), t3 = v * (1.f - s * (1.f - h));
+    // sector_data = {{1,3,0}, {1,0,2}, {3,0,1}, {0,2,1}, {0,1,3}, {2,1,0}} -> (b, g, r)
+    switch (sector) {
+      case 0: b = t1; g = t3; r = t0; break;
+      case 1: b = t1; g = t0; r = t2; break;
+      case 2: b = t3; g = t0; r = t1; break;
+      case 3: b = t0; g = t2; r = t1; break;
+      case 4: b = t0; g = t1; r = t3; break;
+      default: b = t2; g = t1; r = t0; break;
+    }
+  }
+  bgr[0] = sat_u8(b * 255.f);
+  bgr[1] = sat_u8(g * 255.f);
+  bgr[2] = sat_u8(r * 255.f);
+}
+
+// One lane = 4 pixels: 12 B of HSV in, 12 B of BGR out (dword loads/stores), V from the
+// int32 table image or from the pixel's coefficients at (lu, lv).
+template <int K, typename TC, int CL>
+__global__ void __launch_bounds__(256)
+relight_frame_k(const void* __restrict__ src, int basis, int64_t P, double lu, double lv,
+                const uint8_t* __restrict__ hsv, uint8_t* __restrict__ bgr) {
+  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (p0 >= P) return;
+  const int np = P - p0 < 4 ? (int)(P - p0) : 4;
+  uint8_t Vv[4];
+  if constexpr (K == 0) {
+    const int32_t* t = static_cast<const int32_t*>(src);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int32_t x = j < np ? t[p0 + j] : 0;
+      Vv[j] = (uint8_t)(x > 255 ? 255 : (x <= 0 ? 0 : x));  // interactive_relighting.py:35-37
+    }
+  } else {
+    const TC* coef = static_cast<const TC*>(src);
+    TC b[K];
+    basis_eval<TC>(basis, (TC)lu, (TC)lv, b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      TC c[K];
+      const int64_t p = j < np ? p0 + j : p0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) c[k] = (CL == RTI_COEF_PLANAR) ? coef[(int64_t)k * P + p] : coef[p * K + k];
+      Vv[j] = cvt_out<uint8_t>(dot_k<K>(c, b));
+    }
+  }
+  uint8_t in[12], o[12];
+  const uint8_t* hp = hsv + p0 * 3;
+  uint8_t* op = bgr + p0 * 3;
+  const bool full = np == 4 && aligned_to(hp, 4) && aligned_to(op, 4);
+  if (full) {
+    const uint32_t* h4 = reinterpret_cast<const uint32_t*>(hp);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      const uint32_t d = h4[w];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) in[4 * w + i] = (uint8_t)(d >> (8 * i));
+    }
+  } else {
+    for (int i = 0; i < 3 * np; ++i) in[i] = hp[i];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint8_t px[3];
+    hsv2bgr_u8(in[3 * j], in[3 * j + 1], Vv[j], px);  // img[:, :, 2] = values (:37)
+    o[3 * j] = px[0];
+    o[3 * j + 1] = px[1];
+    o[3 * j + 2] = px[2];
+  }
+  if (full) {
+    uint32_t* o4 = reinterpret_cast<uint32_t*>(op);
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+      o4[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
+              ((uint32_t)o[4 * w + 3] << 24);
+  } else {
+    for (int i = 0; i < 3 * np; ++i) op[i] = o[i];
+  }
+}
+
+template <int K, typename TC>
+void launch_frame_cl(const void* src, int basis, int cl, int64_t P, double lu, double lv, const uint8_t* hsv,
+                     uint8_t* bgr, hipStream_t s) {
+  const dim3 grid(grid_1d((P + 3) / 4, 256));
+  if (cl == RTI_COEF_PLANAR)
+    hipLaunchKernelGGL((relight_frame_k<K, TC, RTI_COEF_PLANAR>), grid, dim3(256), 0, s, src, basis, P, lu, lv, hsv,
+                       bgr);
+  else
+    hipLaunchKernelGGL((relight_frame_k<K, TC, RTI_COEF_PIXEL_MAJOR>), grid, dim3(256), 0, s, src, basis, P, lu, lv,
+                       hsv, bgr);
+}
+
+template <typename TC>
+void launch_frame(const void* src, int basis, int cl, int64_t P, double lu, double lv, const uint8_t* hsv,
+                  uint8_t* bgr, hipStream_t s) {
+  switch (basis_terms(basis)) {
+    case 6: launch_frame_cl<6, TC>(src, basis, cl, P, lu, lv, hsv, bgr, s); break;
+    case 9: launch_frame_cl<9, TC>(src, basis, cl, P, lu, lv, hsv, bgr, s); break;
+    default: launch_frame_cl<16, TC>(src, basis, cl, P, lu, lv, hsv, bgr, s); break;
+  }
+}
+
 }  // namespace
 }  // namespace rti
 
@@ -201,4 +330,26 @@ extern "C" int rti_relight(const void* coef, int coef_dtype, int basis, int64_t 
   else
     launch_k<float>(a, out_dtype);
   return check_launch("rti_relight");
+}
+
+extern "C" int rti_relight_frame(const void* src, int src_dtype, int basis, int coef_layout, int64_t P, double lu,
+                                 double lv, const uint8_t* hsv, uint8_t* bgr, rti_stream_t stream) {
+  if (!src || !hsv || !bgr) return fail(RTI_ERR_BAD_ARG, "rti_relight_frame: null pointer");
+  if (P <= 0) return fail(RTI_ERR_BAD_ARG, "rti_relight_frame: P must be positive");
+  hipStream_t s = (hipStream_t)stream;
+  if (src_dtype == RTI_I32) {
+    hipLaunchKernelGGL((relight_frame_k<0, float, RTI_COEF_PIXEL_MAJOR>), dim3(grid_1d((P + 3) / 4, 256)), dim3(256),
+                       0, s, src, basis, P, lu, lv, hsv, bgr);
+    return check_launch("rti_relight_frame");
+  }
+  if (src_dtype != RTI_F32 && src_dtype != RTI_F64)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_relight_frame: src dtype %d", src_dtype);
+  if (basis_terms(basis) < 0) return fail(RTI_ERR_BAD_ARG, "rti_relight_frame: unknown basis %d", basis);
+  if (coef_layout != RTI_COEF_PIXEL_MAJOR && coef_layout != RTI_COEF_PLANAR)
+    return fail(RTI_ERR_BAD_ARG, "rti_relight_frame: coef layout %d", coef_layout);
+  if (src_dtype == RTI_F64)
+    launch_frame<double>(src, basis, coef_layout, P, lu, lv, hsv, bgr, s);
+  else
+    launch_frame<float>(src, basis, coef_layout, P, lu, lv, hsv, bgr, s);
+  return check_launch("rti_relight_frame");
 }

@@ -88,6 +88,8 @@ SIGNATURES = {
                                   _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p]),
     "rti_relight": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_int, _c_void_p, _c_int, _c_void_p, _c_int,
                              _c_int, _c_void_p]),
+    "rti_relight_frame": (_c_int, [_c_void_p, _c_int, _c_int, _c_int, _c_i64, _c_double, _c_double, _c_void_p,
+                                   _c_void_p, _c_void_p]),
 }
 
 _lock = threading.Lock()

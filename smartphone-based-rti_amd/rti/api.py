@@ -282,6 +282,50 @@ def relight(coef, lu, lv, basis="ptm", *, layout="pixel", out_dtype=torch.float3
     return out
 
 
+def relight_frame(src, hsv, lu=None, lv=None, basis="ptm", *, layout="pixel", out=None):
+    """One relighting_event image on the GPU (interactive_relighting.py:31-38):
+    V = clip(value, 0, 255) written into the HSV ROI's V channel, then OpenCV's 8-bit
+    HSV -> BGR conversion, in one launch.
+
+    src: CUDA int32 [H, W] table image (the cursor's interpolation_results[ly][lx]), or
+    fp32/fp64 coefficient maps ([H, W, k] layout="pixel" / [k, H, W] "planar") evaluated at
+    (lu, lv) and truncated to int32 like the reference's tables.
+    hsv: CUDA uint8 [H, W, 3].  Returns (or fills ``out``) CUDA uint8 [H, W, 3] BGR."""
+    _require_cuda(src, "src")
+    _require_cuda(hsv, "hsv")
+    if hsv.dtype != torch.uint8 or hsv.shape[-1] != 3:
+        raise ValueError("hsv must be uint8 [..., 3]")
+    spatial = tuple(hsv.shape[:-1])
+    P = int(np.prod(spatial))
+    if src.dtype == torch.int32:
+        if int(src.numel()) != P:
+            raise ValueError(f"table image has {src.numel()} pixels, hsv has {P}")
+        sdt, b, cl, u, v = L.RTI_I32, L.RTI_BASIS_PTM6, L.RTI_COEF_PIXEL_MAJOR, 0.0, 0.0
+    else:
+        sdt = _COEF_DTYPES.get(src.dtype)
+        if sdt is None:
+            raise ValueError("src must be an int32 table image or float32/float64 coefficients")
+        if lu is None or lv is None:
+            raise ValueError("coefficient maps need a light direction (lu, lv)")
+        b = basis_id(basis)
+        k = basis_terms(b)
+        cl = _layout_id(layout)
+        if int(src.numel()) != P * k:
+            raise ValueError(f"coefficients {tuple(src.shape)} do not match {k} terms x {P} pixels")
+        u, v = float(lu), float(lv)
+    h = hsv.contiguous()
+    c = src.contiguous()
+    if out is None:
+        out = torch.empty(spatial + (3,), dtype=torch.uint8, device=hsv.device)
+    elif out.dtype != torch.uint8 or int(out.numel()) != 3 * P or not out.is_contiguous():
+        raise ValueError("out must be a contiguous uint8 tensor with 3 bytes per pixel")
+    if out.data_ptr() == h.data_ptr():
+        raise ValueError("out may not alias hsv")
+    st = L.lib().rti_relight_frame(_vp(c), sdt, b, cl, P, u, v, _vp(h), _vp(out), _stream_of(h))
+    L.check(st, "rti_relight_frame")
+    return out
+
+
 # ---- light operators (RBF, fused PTM/HSH fit + evaluation) ----------------------------------
 
 def _query(qu, qv):

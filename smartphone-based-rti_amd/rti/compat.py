@@ -13,6 +13,7 @@ interpolate_intensities (PTM)   analysis.py:321-372                          rti
 interpolate_intensities (RBF)   analysis.py:321-372 (default method)         rti_rbf_perpixel, or the shared operator
 prepare_images_data             analysis.py:375-411                          layout adapter (torch); native: relight_tables
 relighting_event lookup         interactive_relighting.py:11-39              table lookup + clip (host, one image)
+relighting_event image          interactive_relighting.py:31-38              RelightingSession: rti_relight_frame
 compute (steps 2-4 + save)      analysis.py:414-482 (from_storage=True)      compute_tables: fused GPU pipeline
 ==============================  ===========================================  ==============================
 
@@ -223,6 +224,56 @@ def relight_at_cursor(coef, x, y, shape, basis="ptm"):
     """Continuous relighting: cursor -> (lx, ly) -> uint8 V image from coefficients."""
     lx, ly = draw_light_roi_position(x, y, shape, to_light_vector=True)
     return api.relight(coef, lx, ly, basis=basis, out_dtype=torch.uint8)
+
+
+class RelightingSession:
+    """interactive_relighting.compute()'s state plus relighting_event (interactive_relighting.py:11-39,
+    78-124) without the OpenCV windows: the HSV ROI (get_ROI(..., hsv=True)) and either the
+    reference's int32 tables ``interpolation_results[ly][lx]`` or coefficient maps stay on the
+    device, and every event is one rti_relight_frame launch (clip + V substitution +
+    HSV -> BGR).
+
+    light_shape: (h, w) of the light-position window the cursor moves in (draw_light, :55-56).
+    With coefficients, ``quantize=True`` evaluates at the 0.02 grid point the reference's table
+    lookup would pick (same image as a table made from the same fp64 coefficients);
+    ``quantize=False`` relights continuously at the cursor's (lx, ly)."""
+
+    def __init__(self, roi_hsv, light_shape, interpolation_results=None, coef=None, basis="ptm", layout="pixel",
+                 quantize=True, device=None):
+        if (interpolation_results is None) == (coef is None):
+            raise ValueError("give exactly one of interpolation_results (int32 tables) or coef (coefficient maps)")
+        self.dev = _device(device)
+        self.hsv = torch.as_tensor(np.ascontiguousarray(roi_hsv, np.uint8)).to(self.dev)
+        self.shape = tuple(light_shape)[:2]
+        self.tables = interpolation_results
+        self.coef = None if coef is None else torch.as_tensor(coef).to(self.dev)
+        self.basis, self.layout, self.quantize = basis, layout, quantize
+        self.axis = grid_axis()
+        self.out = torch.empty(self.hsv.shape, dtype=torch.uint8, device=self.dev)
+        self._table_dev = None
+
+    def light(self, x, y):
+        """draw_light (interactive_relighting.py:42-61) minus the drawing: cursor -> (lx, ly)."""
+        return draw_light_roi_position(x, y, self.shape, to_light_vector=True)
+
+    def frame(self, x, y):
+        """Device uint8 [R, R, 3] BGR image for a cursor position (no host copy)."""
+        lx, ly = self.light(x, y)
+        iy, ix = table_index(ly), table_index(lx)
+        if self.coef is None:
+            t = np.ascontiguousarray(self.tables[iy][ix], np.int32)
+            if self._table_dev is None or self._table_dev.shape != t.shape:
+                self._table_dev = torch.empty(t.shape, dtype=torch.int32, device=self.dev)
+            self._table_dev.copy_(torch.from_numpy(t))
+            return api.relight_frame(self._table_dev, self.hsv, out=self.out)
+        lu, lv = (self.axis[ix], self.axis[iy]) if self.quantize else (lx, ly)
+        return api.relight_frame(self.coef, self.hsv, lu, lv, basis=self.basis, layout=self.layout, out=self.out)
+
+    def relighting_event(self, event, x, y, flags=None, param=None):
+        """interactive_relighting.py:11-39: returns the BGR image the reference passes to imshow.
+
+        Unlike the reference, the table is not clipped in place (a copy is clipped on the GPU)."""
+        return self.frame(x, y).cpu().numpy()
 
 
 def compute_tables(results_frames, interpolate_PTM=False, first_only=False, origin=(0.0, 0.0), device=None):

@@ -130,3 +130,15 @@ def test_rbf_perpixel_default_path_matches_reference():
     assert str(d["singular_raises"]) == "LinAlgError"
     with pytest.raises(np.linalg.LinAlgError):
         o.rbf_linear(d["singular_lx"][0, 0], d["singular_ly"][0, 0], d["I"][0, 0], [0.0], [0.0])
+
+
+def test_hsv2bgr_known_answers():
+    """OpenCV's documented 8-bit HSV (hue range 180) primaries and greys (cvtColor COLOR_HSV2BGR)."""
+    hsv = np.array([[0, 255, 255], [60, 255, 255], [120, 255, 255], [30, 255, 255], [90, 255, 255],
+                    [150, 255, 255], [0, 0, 128], [77, 0, 200], [0, 0, 0], [0, 255, 0]], np.uint8)
+    bgr = np.array([[0, 0, 255], [0, 255, 0], [255, 0, 0], [0, 255, 255], [255, 255, 0],
+                    [255, 0, 255], [128, 128, 128], [200, 200, 200], [0, 0, 0], [0, 0, 0]], np.uint8)
+    assert np.array_equal(o.hsv2bgr_u8(hsv), bgr)
+    # V substitution + clip as relighting_event does (interactive_relighting.py:33-38)
+    img = o.relighting_event_image(np.array([[300, -4]], np.int32), np.array([[[0, 0, 9], [0, 0, 9]]], np.uint8))
+    assert np.array_equal(img, np.array([[[255] * 3, [0] * 3]], np.uint8))
