@@ -32,7 +32,9 @@ __device__ __forceinline__ double ld_d(const T* p) {
 }
 
 // Packed upper triangle of the symmetric 6×6 normal matrix.
-constexpr int tri(int i, int j) { return i <= j ? i * 6 - i * (i - 1) / 2 + (j - i) : tri(j, i); }
+constexpr int tri(int i, int j) {
+  return i <= j ? i * 6 - i * (i - 1) / 2 + (j - i) : j * 6 - j * (j - 1) / 2 + (i - j);
+}
 
 struct Normal6 {
   double m[21];
@@ -46,15 +48,36 @@ __device__ __forceinline__ void ne_zero(Normal6& ne) {
   for (int i = 0; i < 6; ++i) ne.b[i] = 0.0;
 }
 
-// Row (lu², lv², lu·lv, lu, lv, 1.) with fp32 monomials (analysis.py:284-285).
+// Row (lu², lv², lu·lv, lu, lv, 1.) with fp32 monomials (analysis.py:284-285).  The
+// constant column costs adds, not FMAs, and its diagonal entry Σ 1·1 = N is set once
+// before the solve (ne_finish).
 __device__ __forceinline__ void ne_add(Normal6& ne, float lu, float lv, double L) {
-  const double r[6] = {(double)(lu * lu), (double)(lv * lv), (double)(lu * lv), (double)lu, (double)lv, 1.0};
+  const double r[5] = {(double)(lu * lu), (double)(lv * lv), (double)(lu * lv), (double)lu, (double)lv};
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
+  for (int i = 0; i < 5; ++i) {
 #pragma unroll
-    for (int j = i; j < 6; ++j) ne.m[tri(i, j)] = fma(r[i], r[j], ne.m[tri(i, j)]);
+    for (int j = i; j < 5; ++j) ne.m[tri(i, j)] = fma(r[i], r[j], ne.m[tri(i, j)]);
+    ne.m[tri(i, 5)] += r[i];
     ne.b[i] = fma(r[i], L, ne.b[i]);
   }
+  ne.b[5] += L;
+}
+
+__device__ __forceinline__ void ne_finish(Normal6& ne, int N) { ne.m[tri(5, 5)] = (double)N; }
+
+// compute_intensities' direction l = d / ‖d‖ (analysis.py:228-229), components rounded to
+// fp32 (:230-231).  1/‖d‖ is the v_rsq_f64 seed refined by two Newton steps (a few fp64
+// ulps), so the fp32 components equal the correctly rounded quotient except when the fp64
+// value lies within those few ulps of an fp32 rounding midpoint (≈1e-8 of inputs; the
+// fit then moves by ~1e-8 relative).  15 VALU ops instead of sqrt + two IEEE divides.
+__device__ __forceinline__ void light_dir_fast(double dx, double dy, double dz, float& lu, float& lv) {
+  const double d2 = fma(dx, dx, fma(dy, dy, dz * dz));
+  double y = __builtin_amdgcn_rsq(d2);
+  const double h = 0.5 * d2;
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  lu = (float)(dx * y);
+  lv = (float)(dy * y);
 }
 
 // Cholesky solve of (AᵀA) a = Aᵀb.  rcond < 0: singular only at a non-positive
@@ -130,14 +153,11 @@ fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I
   const T* __restrict__ src = I + p;
 #pragma unroll 4
   for (int n = 0; n < N; ++n) {
-    const double dx = cams[3 * n + 0] - px;  // cams: wave-uniform -> scalar loads
-    const double dy = cams[3 * n + 1] - py;
-    const double dz = cams[3 * n + 2];
-    const double nrm = sqrt(dx * dx + dy * dy + dz * dz);
-    const float lu = (float)(dx / nrm);  // float32 lx/ly (analysis.py:217-218, 230-231)
-    const float lv = (float)(dy / nrm);
+    float lu, lv;  // cams: wave-uniform -> scalar loads
+    light_dir_fast(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv);
     ne_add(ne, lu, lv, ld_d(src + (int64_t)n * lstride));
   }
+  ne_finish(ne, N);
   double a[6];
   ne_solve(ne, rcond, a);
   store_coef<TC, LAYOUT>(coef, P, p, a);
@@ -154,6 +174,7 @@ fit_perpixel_dirs(const float* __restrict__ lu, const float* __restrict__ lv, co
   ne_zero(ne);
 #pragma unroll 4
   for (int n = 0; n < N; ++n) ne_add(ne, lu[base + n], lv[base + n], ld_d(I + base + n));
+  ne_finish(ne, N);
   double a[6];
   ne_solve(ne, rcond, a);
   store_coef<TC, LAYOUT>(coef, P, p, a);
