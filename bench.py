@@ -308,7 +308,10 @@ class OperatorWorkload:
         self.qu, self.qv = np.tile(xf, xf.size), np.repeat(xf, xf.size)
         self.E = E = self.qu.size
         self.op64 = rti.rbf_operator(self.lu, self.lv, self.qu, self.qv)  # [N, E] fp64 (host, one-time)
+        self.precision = args.op_precision
         self.op = torch.as_tensor(self.op64.astype(np.float32), device=dev).contiguous()
+        if self.precision == "split16":
+            self.hi, self.lo, self.Kp, self.inv = rti.api.split_operator_f16(self.op64, dev)
         self.out = torch.empty((E, P), dtype=torch.int32, device=dev)
         self.units = P * E
         self.alg_bytes = 4.0 * P * N + 4.0 * P * E  # stack read once + int32 tables written
@@ -323,17 +326,35 @@ class OperatorWorkload:
     def step(self, i):
         c = self.ctypes
         L = self.rti._lib
+        stream = c.c_void_p(torch.cuda.current_stream().cuda_stream)
+        if self.precision == "split16":
+            st = self.lib.rti_apply_operator_f16(c.c_void_p(self.hi.data_ptr()), c.c_void_p(self.lo.data_ptr()),
+                                                 self.Kp, self.inv, self.E, self.N, c.c_void_p(self.I.data_ptr()),
+                                                 L.RTI_F32, self.P, 1, self.P, self.N * self.P,
+                                                 c.c_void_p(self.out.data_ptr()), L.RTI_I32, self.P, self.E * self.P,
+                                                 stream)
+            L.check(st, "rti_apply_operator_f16")
+            return
         st = self.lib.rti_apply_operator(c.c_void_p(self.op.data_ptr()), self.E, self.N, self.E,
                                          c.c_void_p(self.I.data_ptr()), L.RTI_F32, self.P, 1, self.P, self.N * self.P,
-                                         c.c_void_p(self.out.data_ptr()), L.RTI_I32, self.P, self.E * self.P,
-                                         c.c_void_p(torch.cuda.current_stream().cuda_stream))
+                                         c.c_void_p(self.out.data_ptr()), L.RTI_I32, self.P, self.E * self.P, stream)
         L.check(st, "rti_apply_operator")
 
     def config(self):
-        return {"lights": self.N, "evals": self.E, "basis": "rbf-linear", "out": "int32 tables [E][P]"}
+        return {"lights": self.N, "evals": self.E, "basis": "rbf-linear", "out": "int32 tables [E][P]",
+                "operator_precision": self.precision}
 
     def roofline(self, kernel_ms):
         ach = self.flops / (kernel_ms * 1e-3) / 1e12
+        if self.precision == "split16":
+            # two f16 MFMA products per multiply-add put the compute at 2 x 3.2e11 x 1.12 flop per launch
+            # (~0.3 ms at the dense f16 peak), so the E x P int32 table writes (6.4 GB) bound it: HBM roofline
+            gbs = self.alg_bytes / (kernel_ms * 1e-3) / 1e9
+            return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(kernel_ms, 4),
+                    "alg_bytes_per_launch": self.alg_bytes, "alg_flops_per_launch": self.flops,
+                    "mfma_f16_TFLOPs_issued": round(2 * self.flops * (self.Kp / self.N) / (kernel_ms * 1e-3) / 1e12, 1),
+                    "mfma_f16_peak": 2516.6}
         return {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None, "kernel_ms": round(kernel_ms, 4),
                 "alg_flops_per_launch": self.flops, "alg_bytes_per_launch": self.alg_bytes,
@@ -438,6 +459,8 @@ def main():
     ap.add_argument("--nontemporal", action="store_true")
     ap.add_argument("--in-dtype", default="f32", choices=["f32", "u8", "i32"],
                     help="intensity stack type for fit configs (BASELINE's metric is fp32)")
+    ap.add_argument("--op-precision", default="split16", choices=["split16", "fp32"],
+                    help="c7: operator as two fp16 halves on f16 MFMA (default) or fp32 on f32 MFMA")
     ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of the maps")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -535,7 +558,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": {"perpixel": "f32 in / f64 solve", "operator": "f32 (MFMA) -> int32",
+            "dtype": {"perpixel": "f32 in / f64 solve", "operator": ("f32 operator as 2 x f16 (f16 MFMA, f32 accumulate) -> int32"
+                                                       if args.op_precision == "split16" else "f32 (MFMA) -> int32"),
                       "rbf_perpixel": "f64 -> int32"}.get(kind, "f32" if args.in_dtype == "f32"
                                                           else f"{args.in_dtype} in / f32 compute"),
             "data": "synthetic (seeded smooth PTM/HSH coefficient fields + N(0,2) noise, rounded to 0..255, fp32)",

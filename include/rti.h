@@ -159,6 +159,23 @@ int rti_apply_operator(const float* opT, int E, int N, int64_t op_stride,
                        void* out, int out_dtype, int64_t out_row_stride, int64_t out_channel_stride,
                        rti_stream_t stream);
 
+/* ---- split-fp16 operator (v_mfma_f32_32x32x16_f16) -----------------------------------
+ * The same product as rti_apply_operator at the fp16 MFMA rate: the host splits the fp64
+ * operator into two fp16 halves, M·s = hi + lo (s = power of two, max|M·s| < 2^15;
+ * inv_scale = 1/s), row-major [E][Kp] with Kp = N rounded up to 16 (16 <= Kp <= 256) and
+ * zero padding; the device stages each 128-pixel tile of I as fp16 (a per-tile power-of-two
+ * scale for values >= 2^15, plus fp16 remainders when the data is not exact in fp16) and
+ * accumulates hi·I + lo·I (+ hi·I_lo) in fp32.  8-bit intensities are exact.
+ * Accuracy: operator carried to 22 significant bits, fp32 accumulation (as the fp32 path).
+ * op_hi / op_lo: device, 16-byte aligned.  Other arguments as rti_apply_operator. */
+int rti_operator_split_f16(const double* opT, int N, int E, int64_t op_stride, int Kp,
+                           uint16_t* hi, uint16_t* lo, float* inv_scale);
+int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp, float inv_scale,
+                           int E, int N, const void* I, int in_dtype, int64_t P, int C,
+                           int64_t light_stride, int64_t channel_stride,
+                           void* out, int out_dtype, int64_t out_row_stride, int64_t out_channel_stride,
+                           rti_stream_t stream);
+
 /* ---- device: per-pixel linear RBF (the reference's default, with its own geometry) ---
  * interpolate_intensities (analysis.py:350-363) -> _interpolate_RBF (analysis.py:249-260)
  * for every pixel: nodes x_n = (lu[p][n], lv[p][n]) and values I[p][n], PIXEL-major as

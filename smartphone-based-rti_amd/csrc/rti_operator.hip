@@ -20,6 +20,8 @@
 // i.e. 16 MFMAs per pair of 16-byte loads.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <type_traits>
 
@@ -120,6 +122,183 @@ apply_op_mfma(const float* __restrict__ opT, int E, int N, int64_t ostride, cons
   }
 }
 
+// ---- split-fp16 MFMA variant (v_mfma_f32_32x32x16_f16) ----------------------------------
+// The fp32 operator is applied as two fp16 GEMMs: M·s = M_hi + M_lo (host split in fp64,
+// s a power of two putting max|M·s| near 2^15), so M_hi + M_lo carries 22 significant bits.
+// A workgroup stages its 128-pixel tile as fp16 x·t (t a per-tile power of two keeping
+// |x·t| < 2^15; t = 1 for 8-bit data) in LDS, pixel-major with lights contiguous (the B
+// operand's k-run); if any staged value is not exact in fp16 (x·t − hi ≠ 0, e.g. fractional
+// fp32 input) the tile also stages the remainders and adds M_hi·I_lo.  Accumulation is fp32
+// in the MFMA; the result is scaled back by 1/(s·t) (exact).  Integer 8-bit intensities —
+// the reference's V channel — are exact, so it costs two f16 MFMAs (16× the fp32 MFMA rate
+// each) per 32×32×16 block instead of sixteen v_mfma_f32_16x16x4_f32.
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int TP16 = 128;  // pixels per workgroup tile (4 blocks of 32)
+
+template <typename T, typename TO, bool VEC>
+__global__ void __launch_bounds__(256)
+apply_op_f16s(const _Float16* __restrict__ ohi, const _Float16* __restrict__ olo, int Kp, float inv_s, int E, int N,
+              const T* __restrict__ I, int64_t P, int64_t lstride, int64_t cstride, TO* __restrict__ out,
+              int64_t orow, int64_t ocs) {
+  constexpr bool EXACT = std::is_same<T, uint8_t>::value;  // 0..255: exact in fp16, t = 1
+  extern __shared__ __attribute__((aligned(16))) _Float16 sI[];  // [2][TP16][KPITCH]
+  __shared__ float s_red[4];
+  const int KPITCH = Kp + 8;  // 16-B pad between pixel rows
+  _Float16* sIlo = sI + TP16 * KPITCH;
+  const int64_t p0 = (int64_t)blockIdx.x * TP16;
+  const T* __restrict__ src = I + (int64_t)blockIdx.z * cstride;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+  auto load4 = [&](int n, int q4, float (&v)[4]) {
+    const int64_t px = p0 + 4 * q4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = 0.f;
+    if (n >= N) return;
+    const T* sp = src + (int64_t)n * lstride + px;
+    if (VEC && px + 3 < P) {
+      typedef T vec_t __attribute__((ext_vector_type(4)));
+      const vec_t t = __builtin_nontemporal_load(reinterpret_cast<const vec_t*>(sp));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = (float)t[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (px + c < P) v[c] = (float)sp[c];
+    }
+  };
+
+  // tile scale t = 2^-e with max|x|·t < 2^15 (non-finite values pass through as inf/NaN)
+  float t = 1.f;
+  if constexpr (!EXACT) {
+    float m = 0.f;
+    for (int idx = threadIdx.x; idx < N * (TP16 / 4); idx += 256) {
+      float v[4];
+      load4(idx / (TP16 / 4), idx % (TP16 / 4), v);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) m = fmaxf(m, fabsf(v[c]) < INFINITY ? fabsf(v[c]) : 0.f);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) s_red[wave] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
+    int e = 0;
+    if (m >= 32768.f) {
+      frexpf(m, &e);  // m < 2^e
+      e -= 15;
+    }
+    t = ldexpf(1.f, -e);
+  }
+  int need_lo = 0;
+  for (int idx = threadIdx.x; idx < Kp * (TP16 / 4); idx += 256) {
+    const int n = idx / (TP16 / 4), q4 = idx % (TP16 / 4);
+    float v[4];
+    load4(n, q4, v);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float x = v[c] * t;
+      const _Float16 hi = (_Float16)x;
+      sI[(4 * q4 + c) * KPITCH + n] = hi;
+      if constexpr (!EXACT) {
+        const _Float16 lo = (_Float16)(x - (float)hi);
+        sIlo[(4 * q4 + c) * KPITCH + n] = lo;
+        need_lo |= (float)lo != 0.f;
+      }
+    }
+  }
+  if constexpr (!EXACT) need_lo = __syncthreads_or(need_lo);
+  else __syncthreads();
+  const float oscale = inv_s / t;
+
+  const int r = lane & 31, h = lane >> 5;
+  const int nrb = (E + 31) / 32;
+  TO* __restrict__ dst = out + (int64_t)blockIdx.z * ocs;
+  for (int rb = blockIdx.y * 4 + wave; rb < nrb; rb += gridDim.y * 4) {
+    const int arow = rb * 32 + r;
+    const bool aok = arow < E;
+    const _Float16* ah = ohi + (int64_t)(aok ? arow : 0) * Kp + 8 * h;
+    const _Float16* al = olo + (int64_t)(aok ? arow : 0) * Kp + 8 * h;
+    floatx16 acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[b][i] = 0.f;
+    for (int k0 = 0; k0 < Kp; k0 += 16) {
+      half8 a_hi = *reinterpret_cast<const half8*>(ah + k0);
+      half8 a_lo = *reinterpret_cast<const half8*>(al + k0);
+      if (!aok) {
+        a_hi = half8{};
+        a_lo = half8{};
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const half8 bh = *reinterpret_cast<const half8*>(sI + (32 * b + r) * KPITCH + k0 + 8 * h);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_hi, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_lo, bh, acc[b], 0, 0, 0);
+      }
+      if (!EXACT && need_lo) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const half8 bl = *reinterpret_cast<const half8*>(sIlo + (32 * b + r) * KPITCH + k0 + 8 * h);
+          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_hi, bl, acc[b], 0, 0, 0);
+        }
+      }
+    }
+    // D: column (pixel) = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 h
+    // reg outer, pixel block inner: consecutive stores continue the same output row
+    // (4 × 128 B = 512 B contiguous per row), which keeps HBM write pages open
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = rb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int64_t px = p0 + 32 * b + r;
+        // non-temporal: the E×P output streams past the operator, which stays in L2
+        if (row < E && px < P)
+          __builtin_nontemporal_store(cvt_out<TO>(acc[b][reg] * oscale), dst + (int64_t)row * orow + px);
+      }
+    }
+  }
+}
+
+template <typename T, typename TO>
+int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int E, int N, const void* I, int64_t P,
+               int C, int64_t ls, int64_t cs, void* out, int64_t orow, int64_t ocs, bool vec, hipStream_t s) {
+  constexpr bool EXACT = std::is_same<T, uint8_t>::value;
+  const size_t lds = (size_t)(EXACT ? 1 : 2) * TP16 * (Kp + 8) * sizeof(_Float16);
+  const unsigned gx = (unsigned)((P + TP16 - 1) / TP16);
+  const int nwb = (E + 127) / 128;  // 4 waves × 32-row blocks per sweep step
+  const unsigned gy = (unsigned)std::max(1, std::min(nwb, (int)((2048 + gx - 1) / gx)));
+  dim3 grid(gx, gy, C);
+  if (lds > 65536) {
+    auto k = vec ? apply_op_f16s<T, TO, true> : apply_op_f16s<T, TO, false>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return fail(RTI_ERR_HIP, "rti_apply_operator_f16: cannot reserve %zu B of LDS", lds);
+  }
+  if (vec)
+    hipLaunchKernelGGL((apply_op_f16s<T, TO, true>), grid, dim3(256), lds, s, hi, lo, Kp, inv_s, E, N,
+                       static_cast<const T*>(I), P, ls, cs, static_cast<TO*>(out), orow, ocs);
+  else
+    hipLaunchKernelGGL((apply_op_f16s<T, TO, false>), grid, dim3(256), lds, s, hi, lo, Kp, inv_s, E, N,
+                       static_cast<const T*>(I), P, ls, cs, static_cast<TO*>(out), orow, ocs);
+  return check_launch("rti_apply_operator_f16");
+}
+
+template <typename T>
+int launch_f16_out(int odt, const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int E, int N, const void* I,
+                   int64_t P, int C, int64_t ls, int64_t cs, void* out, int64_t orow, int64_t ocs, bool vec,
+                   hipStream_t s) {
+  switch (odt) {
+    case RTI_F32: return launch_f16<T, float>(hi, lo, Kp, inv_s, E, N, I, P, C, ls, cs, out, orow, ocs, vec, s);
+    case RTI_F64: return launch_f16<T, double>(hi, lo, Kp, inv_s, E, N, I, P, C, ls, cs, out, orow, ocs, vec, s);
+    case RTI_I32: return launch_f16<T, int32_t>(hi, lo, Kp, inv_s, E, N, I, P, C, ls, cs, out, orow, ocs, vec, s);
+    default: return launch_f16<T, uint8_t>(hi, lo, Kp, inv_s, E, N, I, P, C, ls, cs, out, orow, ocs, vec, s);
+  }
+}
+
 template <typename T, typename TO>
 int launch(const float* opT, int E, int N, int64_t os, const void* I, int64_t P, int C, int64_t ls, int64_t cs,
            void* out, int64_t orow, int64_t ocs, bool vec, hipStream_t s) {
@@ -183,5 +362,70 @@ extern "C" int rti_apply_operator(const float* opT, int E, int N, int64_t op_str
     case RTI_F32: return launch_out<float>(out_dtype, opT, E, N, os, I, P, C, ls, cs, out, orow, ocs, vec, s);
     case RTI_I32: return launch_out<int32_t>(out_dtype, opT, E, N, os, I, P, C, ls, cs, out, orow, ocs, vec, s);
     default: return launch_out<uint8_t>(out_dtype, opT, E, N, os, I, P, C, ls, cs, out, orow, ocs, vec, s);
+  }
+}
+
+extern "C" int rti_operator_split_f16(const double* opT, int N, int E, int64_t op_stride, int Kp, uint16_t* hi,
+                                      uint16_t* lo, float* inv_scale) {
+  if (!opT || !hi || !lo || !inv_scale) return fail(RTI_ERR_BAD_ARG, "rti_operator_split_f16: null pointer");
+  if (N <= 0 || E <= 0) return fail(RTI_ERR_BAD_ARG, "rti_operator_split_f16: N and E must be positive");
+  if (Kp < N || Kp % 16 != 0) return fail(RTI_ERR_BAD_ARG, "rti_operator_split_f16: Kp must be a multiple of 16 >= N");
+  const int64_t os = op_stride ? op_stride : E;
+  if (os < E) return fail(RTI_ERR_BAD_ARG, "rti_operator_split_f16: op_stride < E");
+  double m = 0.0;
+  for (int n = 0; n < N; ++n)
+    for (int e = 0; e < E; ++e) {
+      const double v = opT[(int64_t)n * os + e];
+      if (!std::isfinite(v)) return fail(RTI_ERR_BAD_ARG, "rti_operator_split_f16: non-finite operator entry");
+      m = std::max(m, std::fabs(v));
+    }
+  int ex = 0;
+  if (m > 0.0) std::frexp(m, &ex);  // m < 2^ex
+  const double sc = std::ldexp(1.0, 15 - ex);  // max|M·s| < 2^15
+  _Float16* H = reinterpret_cast<_Float16*>(hi);
+  _Float16* L = reinterpret_cast<_Float16*>(lo);
+  for (int e = 0; e < E; ++e)
+    for (int n = 0; n < Kp; ++n) {
+      const double v = n < N ? opT[(int64_t)n * os + e] * sc : 0.0;
+      const _Float16 h = (_Float16)v;
+      H[(int64_t)e * Kp + n] = h;
+      L[(int64_t)e * Kp + n] = (_Float16)(v - (double)h);
+    }
+  *inv_scale = (float)(1.0 / sc);
+  return RTI_OK;
+}
+
+extern "C" int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp, float inv_scale, int E,
+                                      int N, const void* I, int in_dtype, int64_t P, int C, int64_t light_stride,
+                                      int64_t channel_stride, void* out, int out_dtype, int64_t out_row_stride,
+                                      int64_t out_channel_stride, rti_stream_t stream) {
+  if (!op_hi || !op_lo || !I || !out) return fail(RTI_ERR_BAD_ARG, "rti_apply_operator_f16: null pointer");
+  if (E <= 0 || N <= 0 || P <= 0 || C <= 0 || C > 65535)
+    return fail(RTI_ERR_BAD_ARG, "rti_apply_operator_f16: bad E/N/P/C");
+  if (Kp < N || Kp % 16 != 0) return fail(RTI_ERR_BAD_ARG, "rti_apply_operator_f16: Kp must be a multiple of 16 >= N");
+  if (Kp > 256) return fail(RTI_ERR_UNSUPPORTED, "rti_apply_operator_f16: N=%d > 256 lights", N);
+  if (in_dtype != RTI_F32 && in_dtype != RTI_U8 && in_dtype != RTI_I32)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_apply_operator_f16: input dtype %d", in_dtype);
+  if (out_dtype != RTI_F32 && out_dtype != RTI_F64 && out_dtype != RTI_I32 && out_dtype != RTI_U8)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_apply_operator_f16: out dtype %d", out_dtype);
+  if (!aligned_to(op_hi, 16) || !aligned_to(op_lo, 16))
+    return fail(RTI_ERR_BAD_ARG, "rti_apply_operator_f16: operator halves must be 16-byte aligned");
+  const int64_t ls = light_stride ? light_stride : P;
+  const int64_t cs = channel_stride ? channel_stride : (int64_t)N * ls;
+  const int64_t orow = out_row_stride ? out_row_stride : P;
+  const int64_t ocs = out_channel_stride ? out_channel_stride : (int64_t)E * orow;
+  if (ls < P || orow < P) return fail(RTI_ERR_BAD_ARG, "rti_apply_operator_f16: stride smaller than extent");
+  const size_t ie = esize(in_dtype);
+  const bool vec = P % 4 == 0 && ls % 4 == 0 && cs % 4 == 0 && aligned_to(I, 4 * ie);
+  const _Float16* hi = reinterpret_cast<const _Float16*>(op_hi);
+  const _Float16* lo = reinterpret_cast<const _Float16*>(op_lo);
+  hipStream_t s = (hipStream_t)stream;
+  switch (in_dtype) {
+    case RTI_F32:
+      return launch_f16_out<float>(out_dtype, hi, lo, Kp, inv_scale, E, N, I, P, C, ls, cs, out, orow, ocs, vec, s);
+    case RTI_I32:
+      return launch_f16_out<int32_t>(out_dtype, hi, lo, Kp, inv_scale, E, N, I, P, C, ls, cs, out, orow, ocs, vec, s);
+    default:
+      return launch_f16_out<uint8_t>(out_dtype, hi, lo, Kp, inv_scale, E, N, I, P, C, ls, cs, out, orow, ocs, vec, s);
   }
 }

@@ -84,6 +84,10 @@ SIGNATURES = {
                                     _c_double_p]),
     "rti_apply_operator": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_void_p, _c_int, _c_i64, _c_int, _c_i64,
                                     _c_i64, _c_void_p, _c_int, _c_i64, _c_i64, _c_void_p]),
+    "rti_operator_split_f16": (_c_int, [_c_double_p, _c_int, _c_int, _c_i64, _c_int, _c_void_p, _c_void_p,
+                                        ctypes.POINTER(ctypes.c_float)]),
+    "rti_apply_operator_f16": (_c_int, [_c_void_p, _c_void_p, _c_int, ctypes.c_float, _c_int, _c_int, _c_void_p, _c_int,
+                                        _c_i64, _c_int, _c_i64, _c_i64, _c_void_p, _c_int, _c_i64, _c_i64, _c_void_p]),
     "rti_rbf_perpixel": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_i64, _c_void_p, _c_int,
                                   _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p]),
     "rti_relight": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_int, _c_void_p, _c_int, _c_void_p, _c_int,

@@ -363,17 +363,38 @@ def basis_operator(lu, lv, qu, qv, basis="ptm", rcond=None):
     return out
 
 
-def apply_operator(opT, I, out_dtype=torch.float32):
+def split_operator_f16(opT, device):
+    """Host split of an fp64 operator opT[N, E] for rti_apply_operator_f16: fp16 halves
+    hi, lo [E, Kp] on ``device`` (M·s = hi + lo, Kp = N rounded up to 16) and 1/s."""
+    op = np.ascontiguousarray(opT.detach().cpu().numpy() if torch.is_tensor(opT) else opT, np.float64)
+    if op.ndim != 2:
+        raise ValueError("operator must be [N, E]")
+    N, E = op.shape
+    Kp = max(16, (N + 15) // 16 * 16)
+    hi = np.empty((E, Kp), np.uint16)
+    lo = np.empty((E, Kp), np.uint16)
+    inv = ctypes.c_float()
+    L.check(L.lib().rti_operator_split_f16(_dptr(op), N, E, E, Kp, hi.ctypes.data_as(ctypes.c_void_p),
+                                           lo.ctypes.data_as(ctypes.c_void_p), ctypes.byref(inv)),
+            "rti_operator_split_f16")
+    return (torch.from_numpy(hi).to(device), torch.from_numpy(lo).to(device), Kp, float(inv.value))
+
+
+def apply_operator(opT, I, out_dtype=torch.float32, precision="auto"):
     """out[.., E, H, W] = Σ_n opT[n, e] · I[.., n, H, W] on the GPU (MFMA).
 
-    opT: [N, E] operator (host array or CUDA tensor; cast to fp32).  I: CUDA
-    [N, H, W], [N, P] or [C, N, H, W], fp32/u8/int32, light-major."""
+    opT: [N, E] operator (host array or tensor).  I: CUDA [N, H, W], [N, P] or
+    [C, N, H, W], fp32/u8/int32, light-major.
+    precision: "split16" (AUTO for N <= 256) = the fp64 operator split into two fp16
+    halves on v_mfma_f32_32x32x16_f16 (22-bit operator, fp32 accumulation);
+    "fp32" = the operator rounded to fp32 on v_mfma_f32_16x16x4_f32."""
     _require_cuda(I, "I")
     odt = _OUT_DTYPES.get(out_dtype)
     if odt is None:
         raise ValueError("out_dtype must be float32, float64, int32 or uint8")
-    op = torch.as_tensor(opT, device=I.device).to(torch.float32).contiguous()
-    N, E = op.shape
+    if precision not in ("auto", "split16", "fp32"):
+        raise ValueError("precision must be 'auto', 'split16' or 'fp32'")
+    N, E = tuple(opT.shape)
     if I.dim() == 2:
         C, spatial = 1, (I.shape[1],)
     elif I.dim() == 3:
@@ -388,9 +409,16 @@ def apply_operator(opT, I, out_dtype=torch.float32):
     P = int(np.prod(spatial))
     Ic = I.contiguous()
     out = torch.empty((C, E) + spatial, dtype=out_dtype, device=I.device)
-    st = L.lib().rti_apply_operator(_vp(op), E, N, E, _vp(Ic), _IN_DTYPES[Ic.dtype], P, C, P, N * P, _vp(out), odt, P,
-                                    E * P, _stream_of(I))
-    L.check(st, "rti_apply_operator")
+    if precision == "split16" or (precision == "auto" and N <= 256):
+        hi, lo, Kp, inv = split_operator_f16(opT, I.device)
+        st = L.lib().rti_apply_operator_f16(_vp(hi), _vp(lo), Kp, inv, E, N, _vp(Ic), _IN_DTYPES[Ic.dtype], P, C, P,
+                                            N * P, _vp(out), odt, P, E * P, _stream_of(I))
+        L.check(st, "rti_apply_operator_f16")
+    else:
+        op = torch.as_tensor(opT, device=I.device).to(torch.float32).contiguous()
+        st = L.lib().rti_apply_operator(_vp(op), E, N, E, _vp(Ic), _IN_DTYPES[Ic.dtype], P, C, P, N * P, _vp(out),
+                                        odt, P, E * P, _stream_of(I))
+        L.check(st, "rti_apply_operator")
     return out if I.dim() == 4 else out[0]
 
 

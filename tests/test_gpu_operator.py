@@ -69,38 +69,74 @@ def test_rbf_singular_raises_linalgerror(cuda):
         rti.rbf_operator(lu, lv, [0.0], [0.0])
 
 
+@pytest.mark.parametrize("precision", ["split16", "fp32"])
 @pytest.mark.parametrize("hw,n,E", [((1, 1), 6, 1), ((3, 5), 7, 3), ((17, 33), 13, 100), ((64, 65), 37, 257),
-                                    ((31, 128), 50, 1000), ((8, 8), 256, 70)])
-def test_operator_ragged_vs_oracle(cuda, hw, n, E):
+                                    ((31, 128), 50, 1000), ((8, 8), 256, 70), ((9, 41), 129, 33)])
+def test_operator_ragged_vs_oracle(cuda, hw, n, E, precision):
     h, w = hw
     lu, lv = o.synth_dirs(n, n)
     I = o.synth_intensities(h, w, lu, lv, seed=h + w)
     rng = np.random.default_rng(E)
     qu, qv = rng.uniform(-1, 1, E), rng.uniform(-1, 1, E)
     op = rti.basis_operator(lu, lv, qu, qv, "ptm")  # fused fit + evaluation
-    out = rti.apply_operator(op, torch.as_tensor(I, device=cuda)).cpu().numpy()
+    out = rti.apply_operator(op, torch.as_tensor(I, device=cuda), precision=precision).cpu().numpy()
     coef = o.fit_shared(I, o.pinv_shared("ptm", lu, lv))
     ref = o.relight(coef, "ptm", qu, qv).reshape(E, h, w)
     err, ok = relight_close(out, ref, rtol=1e-5)
     assert ok, err
 
 
-def test_operator_channels_and_int_outputs(cuda):
+@pytest.mark.parametrize("precision", ["split16", "fp32"])
+def test_operator_channels_and_int_outputs(cuda, precision):
     lu, lv = o.synth_dirs(30, 2)
     planes = np.stack([o.synth_intensities(20, 24, lu, lv, seed=s) for s in (1, 2, 3)])  # [3, N, H, W]
     qu, qv = grid_q()
     op = rti.rbf_operator(lu, lv, qu[:500], qv[:500])
     I = torch.as_tensor(planes, device=cuda)
-    f = rti.apply_operator(op, I, out_dtype=torch.float64).cpu().numpy()
+    f = rti.apply_operator(op, I, out_dtype=torch.float64, precision=precision).cpu().numpy()
     assert f.shape == (3, 500, 20, 24)
     ref = np.einsum("ne,cnhw->cehw", op, planes.astype(np.float64))
     err, ok = relight_close(f, ref)
     assert ok, err
-    i32 = rti.apply_operator(op, I, out_dtype=torch.int32).cpu().numpy()
-    u8 = rti.apply_operator(op, I, out_dtype=torch.uint8).cpu().numpy()
+    i32 = rti.apply_operator(op, I, out_dtype=torch.int32, precision=precision).cpu().numpy()
+    u8 = rti.apply_operator(op, I, out_dtype=torch.uint8, precision=precision).cpu().numpy()
     frac = np.abs(ref - np.round(ref)) > 1e-3
     assert np.array_equal(i32[frac], np.trunc(ref[frac]).astype(np.int32))
     assert np.array_equal(u8[frac], np.clip(np.trunc(ref[frac]), 0, 255).astype(np.uint8))
+
+
+@pytest.mark.parametrize("kind", ["fractional", "large", "int32", "nonfinite"])
+def test_split16_non_fp16_inputs(cuda, kind):
+    """The split-fp16 path stages remainders for inputs not exact in fp16 and scales tiles whose
+    values reach 2^15, so any fp32/int32 stack keeps fp32-level accuracy."""
+    rng = np.random.default_rng(7)
+    n, P, E = 40, 1000, 300
+    lu, lv = o.synth_dirs(n, 3)
+    qu, qv = rng.uniform(-1, 1, E), rng.uniform(-1, 1, E)
+    op = rti.rbf_operator(lu, lv, qu, qv)
+    if kind == "fractional":
+        I = rng.uniform(0, 255, (n, P)).astype(np.float32)
+    elif kind == "large":
+        I = (rng.uniform(0, 1, (n, P)) * np.where(np.arange(P) < 500, 1e6, 3.0)).astype(np.float32)
+    elif kind == "int32":
+        I = rng.integers(-2**30, 2**30, (n, P)).astype(np.int32)
+    else:
+        I = rng.uniform(0, 255, (n, P)).astype(np.float32)
+        I[3, 700] = np.inf
+    ref = op.T @ I.astype(np.float64)
+    out = rti.apply_operator(op, torch.as_tensor(I, device=cuda), out_dtype=torch.float64,
+                             precision="split16").cpu().numpy()
+    if kind == "nonfinite":
+        tile = (np.arange(P) >= 640) & (np.arange(P) < 768)  # the 128-pixel tile holding the inf
+        assert not np.isfinite(out[:, 700]).all()
+        ok = ~tile
+        scale = np.abs(op).sum(0)[:, None] * np.abs(I[:, ok]).max(0)[None, :]
+        assert (np.abs(out[:, ok] - ref[:, ok]) <= 1e-5 * np.maximum(scale, 255)).all()
+        return
+    # fp32-level: |err| <= 1e-5 * Σ_n |M_en| |I_np| (the fp32 path's bound)
+    bound = 1e-5 * (np.abs(op).T @ np.abs(I.astype(np.float64)))
+    err = np.abs(out - ref)
+    assert (err <= np.maximum(bound, 1e-9)).all(), float((err / np.maximum(bound, 1e-9)).max())
 
 
 @pytest.mark.parametrize("out_dtype", [torch.float64, torch.float32])
