@@ -30,7 +30,7 @@ def _worker(rank, world, port, q):
 
     import rti
     import rti_oracle as o
-    from rti.parallel import fit_rowtiled, row_range
+    from rti.parallel import fit_rowtiled, fit_rowtiled_overlapped, row_range
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -44,7 +44,9 @@ def _worker(rank, world, port, q):
         whole = rti.fit(torch.as_tensor(I, device=dev), lu, lv).cpu().numpy()
         ref = o.fit_shared(I, o.pinv_shared("ptm", lu, lv)).reshape(H, W, 6)
         err = float((np.abs(full - ref) / np.abs(ref).max(-1, keepdims=True)).max())
-        q.put((rank, full.shape, bool(np.array_equal(full, whole)), err))
+        over = fit_rowtiled_overlapped(local, lu, lv, H, chunks=3).cpu().numpy()  # chunked fit + all-gather
+        same = bool(np.array_equal(full, whole)) and bool(np.array_equal(over, whole))
+        q.put((rank, full.shape, same, err))
     finally:
         dist.destroy_process_group()
 

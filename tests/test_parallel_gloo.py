@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from rti.parallel import gather_rows, row_range
+from rti.parallel import gather_rows, gather_rows_pipelined, row_range
 
 
 def _free_port():
@@ -66,3 +66,40 @@ def test_gather_rows_two_ranks(H, W):
         assert p.exitcode == 0
     for rank, ok, shape in results:
         assert ok and shape == (H, W, 6), (rank, shape)
+
+
+def _pipelined_worker(rank, world, port, H, W, chunks, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full_ref = torch.arange(H * W * 6, dtype=torch.float32).reshape(H, W, 6)
+        r0, r1 = row_range(H, world, rank)
+        calls = []
+
+        def produce(c0, c1):  # stands in for one fit launch per row chunk
+            calls.append((c0, c1))
+            return full_ref[r0 + c0: r0 + c1].clone()
+
+        full = gather_rows_pipelined(produce, r1 - r0, H, (W, 6), torch.float32, torch.device("cpu"), chunks=chunks)
+        covered = sorted(calls) == calls and sum(b - a for a, b in calls) == r1 - r0
+        q.put((rank, bool(torch.equal(full, full_ref)), covered))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("H,W,chunks,world", [(9, 5, 4, 2), (16, 8, 3, 2), (3, 4, 4, 2), (1, 3, 2, 2), (11, 2, 5, 3)])
+def test_gather_rows_pipelined(H, W, chunks, world):
+    """Chunked all-gather (overlapped with the per-chunk fit on GPUs) reassembles the exact map,
+    including ranks with fewer rows than chunks and ranks with no rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, H, W, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, covered in results:
+        assert ok and covered, rank
