@@ -43,6 +43,9 @@ CONFIGS = {
     "c7": ("operator", 400, 400, 100, 1, "rbf",
            "linear-RBF interpolation (reference default, SciPy Rbf) of a 400x400 ROI x 100 shared lights on the "
            "100x100 grid -> int32 tables (interpolate_intensities + prepare_images_data)"),
+    "c9": ("frame", 2160, 3840, 1000, 1, "ptm",
+           "interactive relight frame 3840x2160 (relighting_event): PTM-6 maps at one cursor (lu,lv) -> int32 -> "
+           "clip -> V of the HSV ROI -> OpenCV HSV2BGR, one launch per event"),
     "c8": ("rbf_perpixel", 400, 400, 100, 1, "rbf",
            "reference default pipeline: per-pixel linear RBF (own light list per pixel, fp64 LU) of a 400x400 ROI x "
            "100 lights on the 100x100 grid -> int32 tables"),
@@ -444,7 +447,52 @@ class RbfPerPixelWorkload:
                           f"evals, {reps} reps in {el:.1f}s; {name}"}
 
 
-WORKLOADS = {"fit": FitWorkload, "relight": RelightWorkload, "perpixel": PerPixelWorkload,
+class FrameWorkload(RelightWorkload):
+    """One step = one rti_relight_frame launch: the image relighting_event shows for one cursor position
+    (interactive_relighting.py:31-38), from device-resident coefficient maps and HSV ROI."""
+
+    def __init__(self, args, cfg, rank, dev):
+        super().__init__(args, cfg, rank, dev)
+        g = torch.Generator(device=dev).manual_seed(2000 + rank)
+        self.hsv = torch.randint(0, 256, (self.P, 3), generator=g, device=dev, dtype=torch.uint8)
+        self.bgr = torch.empty((self.P, 3), dtype=torch.uint8, device=dev)
+        self.luv_host = self.luv.cpu().numpy()
+        self.alg_bytes = 4.0 * self.P * self.k + 3.0 * self.P + 3.0 * self.P  # coefficients + HSV in, BGR out
+
+    def step(self, i):
+        c = self.ctypes
+        lu, lv = self.luv_host[i % self.E]
+        st = self.lib.rti_relight_frame(c.c_void_p(self.coef.data_ptr()), self.rti._lib.RTI_F32, self.bid,
+                                        self.rti._lib.RTI_COEF_PIXEL_MAJOR, self.P, float(lu), float(lv),
+                                        c.c_void_p(self.hsv.data_ptr()), c.c_void_p(self.bgr.data_ptr()),
+                                        c.c_void_p(torch.cuda.current_stream().cuda_stream))
+        self.rti._lib.check(st, "rti_relight_frame")
+
+    def config(self):
+        return {"events": self.E, "basis": self.basis, "k": self.k, "coef_layout": "pixel",
+                "out": "uint8 BGR [P][3]"}
+
+    def cpu_baseline(self, budget_s):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import rti_oracle as o
+
+        rows = max(1, self.H // 10)
+        c = self.coef[: rows * self.W].cpu().numpy()
+        hsv = self.hsv[: rows * self.W].cpu().numpy().reshape(rows, self.W, 3)
+        lu, lv = self.luv_host[0]
+
+        def one():
+            v = o.relight(c, self.basis, lu, lv).reshape(rows, self.W)
+            return o.relighting_event_image(np.trunc(v).astype(np.int32), hsv)
+
+        rate, reps, el = cpu_sample_rate(one, rows * self.W, budget_s)
+        threads, name = cpu_info()
+        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oracle relight + clip + HSV2BGR (NumPy) on {rows}x{self.W} px x 1 event, {reps} reps in "
+                          f"{el:.1f}s; {name}"}
+
+
+WORKLOADS = {"fit": FitWorkload, "relight": RelightWorkload, "perpixel": PerPixelWorkload, "frame": FrameWorkload,
              "operator": OperatorWorkload, "rbf_perpixel": RbfPerPixelWorkload}
 
 
@@ -470,7 +518,7 @@ def main():
     cfg = CONFIGS[args.config]
     kind = cfg[0]
     if args.steps is None:
-        args.steps = {"fit": 20, "relight": 1000, "perpixel": 10, "operator": 10, "rbf_perpixel": 3}[kind]
+        args.steps = {"fit": 20, "relight": 1000, "frame": 1000, "perpixel": 10, "operator": 10, "rbf_perpixel": 3}[kind]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -573,7 +621,7 @@ def main():
             "vs_baseline": None,
             "dtype": {"perpixel": "f32 in / f64 solve", "operator": ("f32 operator as 2 x f16 (f16 MFMA, f32 accumulate) -> int32"
                                                        if args.op_precision == "split16" else "f32 (MFMA) -> int32"),
-                      "rbf_perpixel": "f64 -> int32"}.get(kind, "f32" if args.in_dtype == "f32"
+                      "rbf_perpixel": "f64 -> int32", "frame": "f32 eval -> u8 BGR"}.get(kind, "f32" if args.in_dtype == "f32"
                                                           else f"{args.in_dtype} in / f32 compute"),
             "data": "synthetic (seeded smooth PTM/HSH coefficient fields + N(0,2) noise, rounded to 0..255, fp32)",
             "config": conf,
