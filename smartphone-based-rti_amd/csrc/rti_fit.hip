@@ -91,15 +91,137 @@ __device__ __forceinline__ void store_f32_nt(float* __restrict__ dst, const floa
 template <int K, int VEC>
 constexpr bool stage_ok() { return VEC == 4 && (VEC * K) % 4 == 0 && K <= 9; }
 
+// Lane → pixel map.  A wave owns NC·64·VEC consecutive pixels; lane l's chunk c is the VEC
+// pixels at wave_base + c·64·VEC + l·VEC, so each load instruction of the wave reads 64·VEC
+// contiguous elements of one light plane and the wave's NC loads of a plane cover
+// NC·64·VEC·sizeof(T) contiguous bytes (8 KiB for PTM-6 fp32 at NC = 8).  Long per-wave runs
+// inside each plane are what moves this kernel toward the HBM peak: on MI355X the c3 read
+// stream goes 0.50 → 0.46 ms and the whole fit 0.64 → 0.56 ms from NC = 1 to NC = 8, although
+// NC = 8 needs 256 VGPRs (one wave per SIMD); occupancy does not matter, run length does
+// (profiles/r01_c3_chunk_sweep.log).
+//
 // dynamic LDS: [pinv weights N*KP floats, 16-B aligned][staging 4 waves * 64 lanes * VEC*K floats]
-template <int K, int VEC, typename T, int LAYOUT, int MODE>
-__global__ void __launch_bounds__(256)
-fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P,
-                int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+template <int K, int VEC, int NC, typename T, int LAYOUT, int MODE, bool TAIL>
+__device__ __forceinline__ void fit_valu_body(const float* __restrict__ pinv, int N, const T* __restrict__ I,
+                                              int64_t P, int64_t lstride, float* __restrict__ dst, int64_t pbase,
+                                              int64_t wave_base, const float* lds_w, float* lds_dyn) {
   constexpr bool NT = (MODE & VM_NT) != 0;
   constexpr bool LDSW = (MODE & VM_LDS) != 0;
   constexpr bool NTS = (MODE & VM_NTS) != 0;
-  constexpr bool STAGE = (MODE & VM_STAGE) != 0 && LAYOUT == RTI_COEF_PIXEL_MAJOR && stage_ok<K, VEC>();
+  constexpr bool STAGE =
+      (MODE & VM_STAGE) != 0 && LAYOUT == RTI_COEF_PIXEL_MAJOR && stage_ok<K, VEC>();
+  constexpr int KP = (K + 3) & ~3;
+  constexpr int CH = 64 * VEC;  // elements between a lane's chunks
+  const T* __restrict__ src = I + pbase;
+  // chunk offsets; in the (single) partial wave a chunk past P re-reads chunk 0 and is not stored
+  bool ok[NC];
+  int coff[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    ok[c] = !TAIL || pbase + (int64_t)c * CH < P;
+    coff[c] = ok[c] ? c * CH : 0;
+  }
+
+  float acc[K][NC * VEC];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int v = 0; v < NC * VEC; ++v) acc[k][v] = 0.f;
+
+  auto weight = [&](int k, int n) -> float {
+    if constexpr (LDSW)
+      return lds_w[n * KP + k];  // same address in every lane: broadcast
+    else
+      return pinv[k * N + n];  // wave-uniform -> s_load
+  };
+
+  constexpr int U = (VEC >= 16) ? 4 : 8;            // loads in flight per lane
+  constexpr int UP = U / NC > 0 ? U / NC : 1;        // light planes per step
+  int n = 0;
+  for (; n + UP <= N; n += UP) {
+    float x[UP][NC][VEC];
+#pragma unroll
+    for (int u = 0; u < UP; ++u)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) load_px<T, VEC, NT>(src + (int64_t)(n + u) * lstride + coff[c], x[u][c]);
+#pragma unroll
+    for (int u = 0; u < UP; ++u)
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float w = weight(k, n + u);
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[k][c * VEC + v] = fmaf(w, x[u][c][v], acc[k][c * VEC + v]);
+      }
+  }
+  for (; n < N; ++n) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float x[VEC];
+      load_px<T, VEC, NT>(src + (int64_t)n * lstride + coff[c], x);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float w = weight(k, n);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[k][c * VEC + v] = fmaf(w, x[v], acc[k][c * VEC + v]);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (!ok[c]) continue;
+    const int64_t p0 = pbase + (int64_t)c * CH;
+    if constexpr (LAYOUT == RTI_COEF_PLANAR) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float o[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) o[v] = acc[k][c * VEC + v];
+        store_f32_nt<VEC, NTS>(dst + (int64_t)k * P + p0, o);
+      }
+    } else {
+      float o[VEC * K];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+#pragma unroll
+        for (int k = 0; k < K; ++k) o[v * K + k] = acc[k][c * VEC + v];
+      if constexpr (STAGE) {
+        constexpr int F = VEC * K;  // floats per lane (24 for PTM-6)
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int64_t cbase = wave_base + (int64_t)c * CH;  // the wave's first pixel of chunk c
+        if (cbase + CH <= P) {  // wave-uniform: the whole chunk's 64*F floats are in range
+          const int woff = LDSW ? ((N * KP + 3) & ~3) : 0;
+          float* st = lds_dyn + woff + wave * 64 * F;
+#pragma unroll
+          for (int i = 0; i < F; i += 4)
+            *reinterpret_cast<floatx4*>(st + lane * F + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          float* wdst = dst + cbase * K;
+#pragma unroll
+          for (int j = 0; j < F / 4; ++j) {
+            const floatx4 t = *reinterpret_cast<const floatx4*>(st + j * 256 + lane * 4);
+            if constexpr (NTS)
+              __builtin_nontemporal_store(t, reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4));
+            else
+              *reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4) = t;
+          }
+          continue;
+        }
+      }
+      store_f32_nt<VEC * K, NTS>(dst + p0 * K, o);
+    }
+  }
+}
+
+template <int K, int VEC, int NC, typename T, int LAYOUT, int MODE>
+__global__ void __launch_bounds__(256)
+fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P,
+                int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  constexpr bool LDSW = (MODE & VM_LDS) != 0;
   constexpr int KP = (K + 3) & ~3;
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   float* lds_w = lds_dyn;
@@ -110,86 +232,16 @@ fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, 
     }
     __syncthreads();
   }
-  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
-  if (p0 >= P) return;
-  const T* __restrict__ src = I + (int64_t)blockIdx.y * cstride + p0;
-
-  float acc[K][VEC];
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) acc[k][v] = 0.f;
-
-  auto weight = [&](int k, int n) -> float {
-    if constexpr (LDSW)
-      return lds_w[n * KP + k];  // same address in every lane: broadcast
-    else
-      return pinv[k * N + n];  // wave-uniform -> s_load
-  };
-
-  constexpr int U = (VEC >= 16) ? 4 : 8;  // light planes in flight per lane
-  int n = 0;
-  for (; n + U <= N; n += U) {
-    float x[U][VEC];
-#pragma unroll
-    for (int u = 0; u < U; ++u) load_px<T, VEC, NT>(src + (int64_t)(n + u) * lstride, x[u]);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float w = weight(k, n + u);
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) acc[k][v] = fmaf(w, x[u][v], acc[k][v]);
-      }
-  }
-  for (; n < N; ++n) {
-    float x[VEC];
-    load_px<T, VEC, NT>(src + (int64_t)n * lstride, x);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const float w = weight(k, n);
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) acc[k][v] = fmaf(w, x[v], acc[k][v]);
-    }
-  }
-
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t wave_base = ((int64_t)blockIdx.x * 4 + wave) * (64 * VEC * NC);
+  const int64_t pbase = wave_base + (int64_t)lane * VEC;
+  if (pbase >= P) return;
+  const T* __restrict__ Ic = I + (int64_t)blockIdx.y * cstride;
   float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
-  if constexpr (LAYOUT == RTI_COEF_PLANAR) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) store_f32_nt<VEC, NTS>(dst + (int64_t)k * P + p0, acc[k]);
-  } else {
-    float o[VEC * K];
-#pragma unroll
-    for (int v = 0; v < VEC; ++v)
-#pragma unroll
-      for (int k = 0; k < K; ++k) o[v * K + k] = acc[k][v];
-    if constexpr (STAGE) {
-      constexpr int F = VEC * K;  // floats per lane (24 for PTM-6)
-      const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-      const int64_t wp0 = ((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63)) * VEC;  // wave's first pixel
-      if (wp0 + 64 * VEC <= P) {  // wave-uniform: the whole wave's 64*F floats are in range
-        const int woff = LDSW ? ((N * KP + 3) & ~3) : 0;
-        float* st = lds_dyn + woff + wave * 64 * F;
-#pragma unroll
-        for (int i = 0; i < F; i += 4)
-          *reinterpret_cast<floatx4*>(st + lane * F + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        float* wdst = dst + wp0 * K;
-#pragma unroll
-        for (int j = 0; j < F / 4; ++j) {
-          const floatx4 t = *reinterpret_cast<const floatx4*>(st + j * 256 + lane * 4);
-          if constexpr (NTS)
-            __builtin_nontemporal_store(t, reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4));
-          else
-            *reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4) = t;
-        }
-        return;
-      }
-    }
-    store_f32_nt<VEC * K, NTS>(dst + p0 * K, o);
-  }
+  if (NC == 1 || wave_base + (int64_t)(64 * VEC * NC) <= P)  // wave-uniform
+    fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, false>(pinv, N, Ic, P, lstride, dst, pbase, wave_base, lds_w, lds_dyn);
+  else
+    fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, true>(pinv, N, Ic, P, lstride, dst, pbase, wave_base, lds_w, lds_dyn);
 }
 
 // ---- MFMA kernel (k <= 16) ------------------------------------------------------------
@@ -294,28 +346,62 @@ struct FitArgs {
   int64_t ocstride;
   bool nt;
   int mode;  // VALU variant bits (VM_*)
+  int nc;    // VALU chunks per lane (1 = one VEC-pixel group per lane)
   hipStream_t stream;
 };
 
-template <int K, int VEC, typename T, int LAYOUT, int MODE>
+template <int K, int VEC, int NC, typename T, int LAYOUT, int MODE>
 void launch_valu_t(const FitArgs& a) {
-  const int64_t groups = (a.P + VEC - 1) / VEC;
+  const int64_t groups = (a.P + VEC * NC - 1) / (VEC * NC);
   dim3 grid(grid_1d(groups, 256), a.C);
   constexpr int KP = (K + 3) & ~3;
   size_t lds = (MODE & VM_LDS) ? (((size_t)a.N * KP + 3) & ~(size_t)3) * sizeof(float) : 0;
   if constexpr ((MODE & VM_STAGE) && LAYOUT == RTI_COEF_PIXEL_MAJOR && stage_ok<K, VEC>())
     lds += (size_t)4 * 64 * VEC * K * sizeof(float);
-  hipLaunchKernelGGL((fit_shared_valu<K, VEC, T, LAYOUT, MODE>), grid, dim3(256), lds, a.stream, a.pinv, a.N,
+  hipLaunchKernelGGL((fit_shared_valu<K, VEC, NC, T, LAYOUT, MODE>), grid, dim3(256), lds, a.stream, a.pinv, a.N,
                      static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride);
+}
+
+// chunks per lane instantiated per k (accumulators K*NC*VEC must fit the 256 VGPRs of a wave)
+template <int K>
+constexpr int nc_max() { return K <= 6 ? 8 : (K <= 9 ? 4 : 3); }
+
+template <int K, int VEC, int NC, typename T, int LAYOUT>
+void launch_valu_ncm(const FitArgs& a) {
+  const int m = a.mode & (VM_NT | VM_NTS | VM_STAGE);
+  if (m == (VM_NT | VM_NTS)) launch_valu_t<K, VEC, NC, T, LAYOUT, VM_NT | VM_NTS>(a);
+  else if (m == (VM_NT | VM_STAGE)) launch_valu_t<K, VEC, NC, T, LAYOUT, VM_NT | VM_STAGE>(a);
+  else if (m & VM_NT) launch_valu_t<K, VEC, NC, T, LAYOUT, VM_NT>(a);
+  else if (m == VM_NTS) launch_valu_t<K, VEC, NC, T, LAYOUT, VM_NTS>(a);
+  else launch_valu_t<K, VEC, NC, T, LAYOUT, 0>(a);
+}
+
+template <int K, int VEC, typename T, int LAYOUT>
+void launch_valu_nc(const FitArgs& a) {
+  // u8 lanes already hold 16 pixels (VEC = 16): at most 2 chunks
+  constexpr int MAXC = VEC >= 16 ? (K <= 6 ? 2 : 1) : nc_max<K>();
+  const int nc = a.nc < MAXC ? a.nc : MAXC;
+  if constexpr (MAXC >= 8) if (nc >= 8) return launch_valu_ncm<K, VEC, 8, T, LAYOUT>(a);
+  if constexpr (MAXC >= 4) if (nc >= 4) return launch_valu_ncm<K, VEC, 4, T, LAYOUT>(a);
+  if constexpr (MAXC >= 3) if (nc == 3) return launch_valu_ncm<K, VEC, 3, T, LAYOUT>(a);
+  if constexpr (MAXC >= 2) if (nc >= 2) return launch_valu_ncm<K, VEC, 2, T, LAYOUT>(a);
+  launch_valu_ncm<K, VEC, 1, T, LAYOUT>(a);
 }
 
 template <int K, int VEC, typename T, int LAYOUT>
 void launch_valu_m(const FitArgs& a) {
+  // wide lanes (NC > 1 chunks per lane): non-temporal or plain loads, plain or NT stores
+  if constexpr (VEC > 1) {
+    if (a.nc > 1) {
+      launch_valu_nc<K, VEC, T, LAYOUT>(a);
+      return;
+    }
+  }
   // every mode for the fp32 16-byte path; the default mode for the others
   if constexpr (VEC > 1 && std::is_same<T, float>::value) {
     switch (a.mode & 15) {
 #define RTI_MODE_CASE(m) \
-  case m: launch_valu_t<K, VEC, T, LAYOUT, m>(a); break;
+  case m: launch_valu_t<K, VEC, 1, T, LAYOUT, m>(a); break;
       RTI_MODE_CASE(0) RTI_MODE_CASE(1) RTI_MODE_CASE(2) RTI_MODE_CASE(3) RTI_MODE_CASE(4) RTI_MODE_CASE(5)
       RTI_MODE_CASE(6) RTI_MODE_CASE(7) RTI_MODE_CASE(8) RTI_MODE_CASE(9) RTI_MODE_CASE(10) RTI_MODE_CASE(11)
       RTI_MODE_CASE(12) RTI_MODE_CASE(13) RTI_MODE_CASE(14) RTI_MODE_CASE(15)
@@ -323,9 +409,9 @@ void launch_valu_m(const FitArgs& a) {
     }
   } else {
     if (a.mode & VM_NT)
-      launch_valu_t<K, VEC, T, LAYOUT, VM_NT>(a);
+      launch_valu_t<K, VEC, 1, T, LAYOUT, VM_NT>(a);
     else
-      launch_valu_t<K, VEC, T, LAYOUT, 0>(a);
+      launch_valu_t<K, VEC, 1, T, LAYOUT, 0>(a);
   }
 }
 
@@ -419,6 +505,7 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
   a.mode = (a.nt ? VM_NT : 0) | ((kernel & RTI_KERNEL_PINV_LDS) ? VM_LDS : 0) |
            ((kernel & RTI_KERNEL_NT_STORE) ? VM_NTS : 0) | ((kernel & RTI_KERNEL_STAGE) ? VM_STAGE : 0);
   if ((a.mode & VM_LDS) && (size_t)N * 16 * sizeof(float) > 24576) a.mode &= ~VM_LDS;  // keep LDS <= 64 KiB
+  a.nc = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;  // 0 = AUTO below
   a.stream = (hipStream_t)stream;
   if (a.lstride < P) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: light_stride < P");
   if (C > 1 && a.cstride < (int64_t)N * a.lstride) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: channel_stride");
@@ -440,10 +527,29 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     use_mfma = false;
   } else {
     // AUTO: measured best on MI355X (profiles/): the VALU stream with
-    // non-temporal intensity loads, SGPR weights and plain coefficient stores.
+    // non-temporal intensity loads and SGPR weights.
     use_mfma = !valu_k;
     a.nt = true;
-    a.mode = VM_NT;
+    // PTM-6 pixel-major coefficients leave through LDS as whole 1 KiB rows per store
+    // instruction: with wide lanes the direct 96-B-strided stores raised WRITE_SIZE to 1.46x
+    // the coefficient bytes (c3 0.573 -> 0.549 ms, c2 0.082 -> 0.072 ms staged)
+    a.mode = VM_NT | (k == 6 ? VM_STAGE : 0);
+  }
+  if (a.nc == 0) {
+    // AUTO chunks per lane (PTM-6, 4-byte intensities): the longest per-wave run in each
+    // plane whose accumulators fit, as long as the launch keeps >= 2000 waves (≈2 per SIMD;
+    // c2 is faster at 4 chunks than at 8).  HSH-16 measured no gain (c4: 3.88 ms at 1 and 2
+    // chunks, 4.57 at 3) and keeps one chunk, as do the LDS-weight tuning variants.
+    const bool plain = (a.mode & ~(VM_NT | VM_NTS | VM_STAGE)) == 0;
+    a.nc = 1;
+    if (plain && in_dtype != RTI_U8 && k == 6) {
+      const int64_t groups = P * C / 4;  // 4-pixel lane groups
+      for (int nc = 8; nc > 1; nc >>= 1)
+        if (groups / (64 * nc) >= 2000) {
+          a.nc = nc;
+          break;
+        }
+    }
   }
   const bool mfma_ok = N <= 1024 && P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 &&
                        aligned_to(I, 4 * es) && aligned_to(coef, 16) && a.ocstride % 4 == 0;

@@ -42,6 +42,7 @@ RTI_KERNEL_NONTEMPORAL = 0x100
 RTI_KERNEL_PINV_LDS = 0x200
 RTI_KERNEL_NT_STORE = 0x400
 RTI_KERNEL_STAGE = 0x800
+RTI_KERNEL_CHUNKS_SHIFT = 12  # VALU chunks per lane in bits 12-15 (0 = AUTO)
 
 
 class RTILibraryMissing(ImportError):

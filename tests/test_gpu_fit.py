@@ -162,3 +162,33 @@ def test_full_size_4k_n100_properties(cuda, kernel):
     coef2 = rti.fit((2 * I + 3).reshape(N, H, W), lu, lv, kernel=kernel, layout="planar").reshape(6, -1)
     c3 = torch.as_tensor(o.pinv_shared("ptm", lu, lv).sum(1) * 3, device=cuda, dtype=torch.float32)[:, None]
     assert float(((coef2 - 2 * coef - c3).abs() / (2 * scale)).max()) < 1e-4
+
+
+@pytest.mark.parametrize("chunks", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("basis,n", [("ptm", 23), ("hsh9", 17), ("hsh", 29)])
+@pytest.mark.parametrize("in_dtype", [torch.float32, torch.uint8, torch.int32])
+def test_wide_lane_chunks(cuda, chunks, basis, n, in_dtype):
+    """VALU kernel with `chunks` 1 KiB runs per lane and plane (RTI_KERNEL_CHUNKS): pixel counts
+    around whole-wave multiples (partial last wave, lanes with only some chunks in range),
+    two channels, both coefficient layouts."""
+    k = rti.basis_terms(basis)
+    lu, lv = o.synth_dirs(n, 31)
+    A = o.design("hsh" if basis != "ptm" else "ptm", lu, lv)[:, :k]
+    pinv64 = np.linalg.pinv(A)
+    pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=cuda)
+    wave_px = 64 * 4 * chunks
+    for P in (4, wave_px - 4, wave_px, wave_px + 4, 3 * wave_px + 260, 5 * wave_px + 1024 * 3 + 8):
+        rng = np.random.default_rng(P + n)
+        I = rng.integers(0, 256, size=(2, n, P)).astype(np.float32)
+        ref = np.einsum("kn,cnp->cpk", pinv64, I.astype(np.float64))
+        Id = torch.as_tensor(I, device=cuda).to(in_dtype)
+        for layout in ("pixel", "planar"):
+            coef = torch.full((2, P, k) if layout == "pixel" else (2, k, P), float("nan"), device=cuda)
+            rti.fit_shared_into(pv, Id, coef, k=k, layout=layout, kernel="valu",
+                                flags=0x100 | (chunks << rti._lib.RTI_KERNEL_CHUNKS_SHIFT))
+            got = coef.cpu().numpy()
+            if layout == "planar":
+                got = np.moveaxis(got, 1, 2)
+            for c in range(2):
+                err, ok = coef_close(got[c], ref[c])
+                assert ok, (P, layout, c, err)

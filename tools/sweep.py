@@ -48,6 +48,9 @@ def main():
         fl = (rti._lib.RTI_KERNEL_NONTEMPORAL if "nt" in opts else 0) | \
              (rti._lib.RTI_KERNEL_PINV_LDS if "lds" in opts else 0) | \
              (rti._lib.RTI_KERNEL_NT_STORE if "nts" in opts else 0) | (rti._lib.RTI_KERNEL_STAGE if "stage" in opts else 0)
+        for o in opts:  # c<n>: chunks per lane (rti.h RTI_KERNEL_CHUNKS)
+            if o[:1] == "c" and o[1:].isdigit():
+                fl |= int(o[1:]) << 12
         variants.append((v, parts[0], parts[1], fl))
     probe = None
     plib = os.path.join(ROOT, "tools", "probe", "libhbm_probe.so")
