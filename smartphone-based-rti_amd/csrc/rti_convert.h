@@ -13,7 +13,8 @@ template <typename TC>
 __device__ __forceinline__ int32_t trunc_i32(TC v) {
   // C truncation toward zero; NaN / out of range -> INT32_MIN (x86 cvttsd2si,
   // which is what NumPy's float64 -> int32 element assignment produces).
-  return (v >= TC(-2147483648.0) && v < TC(2147483648.0)) ? (int32_t)v : INT32_MIN;
+  // (|v| < 2^31 is the same test: v = -2^31 converts to INT32_MIN either way; one compare)
+  return (v < TC(2147483648.0) && -v < TC(2147483648.0)) ? (int32_t)v : INT32_MIN;
 }
 
 template <typename TO, typename TC>

@@ -136,10 +136,11 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int TP16 = 128;  // pixels per workgroup tile (4 blocks of 32)
+constexpr int KSMAX = 8;   // k-steps (16 lights each) the pipelined sweep holds in registers: N <= 128
 
 template <typename T, typename TO, bool VEC>
 __global__ void __launch_bounds__(256)
-apply_op_f16s(const _Float16* __restrict__ ohi, const _Float16* __restrict__ olo, int Kp, float inv_s, int E, int N,
+apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int E, int N,
               const T* __restrict__ I, int64_t P, int64_t lstride, int64_t cstride, TO* __restrict__ out,
               int64_t orow, int64_t ocs) {
   constexpr bool EXACT = std::is_same<T, uint8_t>::value;  // 0..255: exact in fp16, t = 1
@@ -215,16 +216,106 @@ apply_op_f16s(const _Float16* __restrict__ ohi, const _Float16* __restrict__ olo
   const int r = lane & 31, h = lane >> 5;
   const int nrb = (E + 31) / 32;
   TO* __restrict__ dst = out + (int64_t)blockIdx.z * ocs;
-  for (int rb = blockIdx.y * 4 + wave; rb < nrb; rb += gridDim.y * 4) {
+  const int ksteps = Kp / 16;
+  const int rb0 = blockIdx.y * 4 + wave, rbstep = gridDim.y * 4;
+
+  // A operand of one 32-row block: lane (r, h) holds operator row rb*32 + r, k-offset 8h of
+  // every 16-wide k-step, hi and lo halves.  Branch-free: k-steps past Kp re-read the last one
+  // (their MFMAs are skipped) and rows past E read row 0 (never stored).
+  auto load_a = [&](int rb, half8 (&ah)[KSMAX], half8 (&al)[KSMAX]) {
+    const int arow = rb * 32 + r;
+    const int64_t rowoff = (int64_t)(arow < E ? arow : 0) * Kp + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KSMAX; ++s) {
+      const int ss = s < ksteps ? s : ksteps - 1;
+      ah[s] = *reinterpret_cast<const half8*>(ohi + rowoff + 16 * ss);
+      al[s] = *reinterpret_cast<const half8*>(olo + rowoff + 16 * ss);
+    }
+  };
+  auto mfma_block = [&](floatx16 (&acc)[4], const half8& a_hi, const half8& a_lo, int k0) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const half8 bh = *reinterpret_cast<const half8*>(sI + (32 * b + r) * KPITCH + k0 + 8 * h);
+      acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_hi, bh, acc[b], 0, 0, 0);
+      acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_lo, bh, acc[b], 0, 0, 0);
+    }
+    if (!EXACT && need_lo) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const half8 bl = *reinterpret_cast<const half8*>(sIlo + (32 * b + r) * KPITCH + k0 + 8 * h);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_hi, bl, acc[b], 0, 0, 0);
+      }
+    }
+  };
+  // D: column (pixel) = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 h
+  // reg outer, pixel block inner: consecutive stores continue the same output row
+  // (4 × 128 B = 512 B contiguous per row), which keeps HBM write pages open.
+  // Non-temporal: the E×P output streams past the operator, which stays in L2.
+  auto store_block = [&](const floatx16 (&acc)[4], int rb, bool guard) {
+    // lane base: row rb*32 + 4h, pixel p0 + r; the 16 row offsets are wave-uniform multiples of orow
+    TO* __restrict__ lb = dst + (int64_t)(rb * 32 + 4 * h) * orow + p0 + r;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int dr = (reg & 3) + 8 * (reg >> 2);
+      const int row = rb * 32 + dr + 4 * h;
+      TO* __restrict__ rp = lb + (int64_t)dr * orow;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (!guard || (row < E && p0 + 32 * b + r < P))
+          __builtin_nontemporal_store(cvt_out<TO>(acc[b][reg] * oscale), rp + 32 * b);
+      }
+    }
+  };
+  auto zero = [](floatx16 (&acc)[4]) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[b][i] = 0.f;
+  };
+
+  int rb = rb0;
+  const int nfull = E / 32;  // row blocks with all 32 rows in range
+  if (ksteps <= KSMAX && p0 + TP16 <= P && rb < nfull) {
+    // Software-pipelined sweep over whole row blocks of a whole pixel tile.  The next block's
+    // operator rows are loaded BEFORE this block's 64 stores are issued: CDNA's single vmcnt
+    // counter retires loads and stores in order, so a load issued after the stores cannot be
+    // waited for without also waiting for every one of them -- which serialised the MFMAs
+    // behind the table writes (c7 1.63 ms against a 0.99 ms store-only floor,
+    // tools/sweep_store.py).  Loads and stores here are branch-free straight-line code, and the
+    // first block is peeled, so the loop header sees the same outstanding-op pattern (16 loads
+    // then 64 stores) from both edges and the compiler's waits stop at the loads.
+    half8 ah[KSMAX], al[KSMAX];
+    floatx16 acc[4];
+    load_a(rb, ah, al);
+    zero(acc);
+#pragma unroll
+    for (int s = 0; s < KSMAX; ++s)
+      if (s < ksteps) mfma_block(acc, ah[s], al[s], 16 * s);
+    int nxt = rb + rbstep < nfull ? rb + rbstep : rb;
+    load_a(nxt, ah, al);
+    __asm__ volatile("" ::: "memory");  // keep every load ahead of the stores (IR and
+    __builtin_amdgcn_sched_barrier(0);  // machine scheduler)
+    store_block(acc, rb, false);
+    for (rb += rbstep; rb < nfull; rb += rbstep) {
+      zero(acc);
+#pragma unroll
+      for (int s = 0; s < KSMAX; ++s)
+        if (s < ksteps) mfma_block(acc, ah[s], al[s], 16 * s);
+      nxt = rb + rbstep < nfull ? rb + rbstep : rb;
+      load_a(nxt, ah, al);
+      __asm__ volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      store_block(acc, rb, false);
+    }
+  }
+  // the rest (partial tile or row block, or N > 16·KSMAX): one block at a time, guarded stores
+  for (; rb < nrb; rb += rbstep) {
     const int arow = rb * 32 + r;
     const bool aok = arow < E;
     const _Float16* ah = ohi + (int64_t)(aok ? arow : 0) * Kp + 8 * h;
     const _Float16* al = olo + (int64_t)(aok ? arow : 0) * Kp + 8 * h;
     floatx16 acc[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[b][i] = 0.f;
+    zero(acc);
     for (int k0 = 0; k0 < Kp; k0 += 16) {
       half8 a_hi = *reinterpret_cast<const half8*>(ah + k0);
       half8 a_lo = *reinterpret_cast<const half8*>(al + k0);
@@ -232,34 +323,9 @@ apply_op_f16s(const _Float16* __restrict__ ohi, const _Float16* __restrict__ olo
         a_hi = half8{};
         a_lo = half8{};
       }
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const half8 bh = *reinterpret_cast<const half8*>(sI + (32 * b + r) * KPITCH + k0 + 8 * h);
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_hi, bh, acc[b], 0, 0, 0);
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_lo, bh, acc[b], 0, 0, 0);
-      }
-      if (!EXACT && need_lo) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const half8 bl = *reinterpret_cast<const half8*>(sIlo + (32 * b + r) * KPITCH + k0 + 8 * h);
-          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_hi, bl, acc[b], 0, 0, 0);
-        }
-      }
+      mfma_block(acc, a_hi, a_lo, k0);
     }
-    // D: column (pixel) = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 h
-    // reg outer, pixel block inner: consecutive stores continue the same output row
-    // (4 × 128 B = 512 B contiguous per row), which keeps HBM write pages open
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = rb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int64_t px = p0 + 32 * b + r;
-        // non-temporal: the E×P output streams past the operator, which stays in L2
-        if (row < E && px < P)
-          __builtin_nontemporal_store(cvt_out<TO>(acc[b][reg] * oscale), dst + (int64_t)row * orow + px);
-      }
-    }
+    store_block(acc, rb, true);
   }
 }
 
