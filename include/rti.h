@@ -62,6 +62,7 @@ extern "C" {
 #define RTI_KERNEL_AUTO 0
 #define RTI_KERNEL_VALU 1   /* pinv in SGPRs, fp32 FMA stream */
 #define RTI_KERNEL_MFMA 2   /* v_mfma_f32_16x16x4_f32, pinv staged in LDS */
+#define RTI_KERNEL_TILE 3   /* the same MFMA fed from a double-buffered LDS tile [4·sp lights][256·rc pixels] */
 /* OR-able tuning flags (VALU kernel; only NONTEMPORAL applies to the MFMA kernel) */
 #define RTI_KERNEL_NONTEMPORAL 0x100  /* non-temporal intensity loads (the stack is read once) */
 #define RTI_KERNEL_PINV_LDS    0x200  /* stage pinv in LDS instead of scalar loads */
@@ -70,6 +71,14 @@ extern "C" {
 /* VALU chunks per lane (bits 12-15; 0 = AUTO): a wave reads chunks*1 KiB contiguous per plane */
 #define RTI_KERNEL_CHUNKS_SHIFT 12
 #define RTI_KERNEL_CHUNKS(n)   ((n) << RTI_KERNEL_CHUNKS_SHIFT)
+/* TILE kernel: CHUNKS(rc) sets the tile width (256·rc pixels; 0 = 8, or 4 above N = 512),
+ * TILE_PLANES(sp) the light planes each wave loads per step (bits 16-19, 0 = 2) */
+#define RTI_KERNEL_TILE_PLANES_SHIFT 16
+#define RTI_KERNEL_TILE_PLANES(n)    ((n) << RTI_KERNEL_TILE_PLANES_SHIFT)
+/* TILE kernel: tiles in the LDS ring (bits 20-23; 0 = 2): 2 = register-staged double buffer,
+ * 3 or 4 = global_load_lds ring with depth-1 steps in flight (fp32 stacks) */
+#define RTI_KERNEL_TILE_DEPTH_SHIFT 20
+#define RTI_KERNEL_TILE_DEPTH(n)    ((n) << RTI_KERNEL_TILE_DEPTH_SHIFT)
 
 typedef void* rti_stream_t; /* hipStream_t */
 

@@ -334,6 +334,223 @@ fit_shared_mfma(const float* __restrict__ pinv, int k, int N, const T* __restric
   }
 }
 
+// ---- LDS-tiled MFMA stream (BASELINE configs[3]: HSH-16 "MFMA 16×N LDS tile") --------------
+// A workgroup owns R = 256·RC consecutive pixels of one channel and sweeps the N lights in
+// steps of S = 4·SP planes.  Per step wave w loads planes w·SP .. w·SP+SP-1 of the tile whole
+// (RC 16-byte loads per lane and plane, so each wave reads R·4 contiguous bytes of every plane
+// it touches: the per-wave run length that moved the PTM stream from 0.64 to 0.55 ms,
+// DESIGN.md §4.1) and parks them in a double-buffered LDS tile [2][S][R].  After one barrier
+// each wave reads its quarter of the pixels back as B operands of v_mfma_f32_16x16x4_f32; A is
+// the pseudo-inverse, staged once per workgroup in LDS as [Npad][16] with rows >= k and padded
+// lights zero.  The next step's loads are issued before the current step's MFMAs (split
+// staging), so their HBM latency hides under the compute, and every byte of I is read once.
+// B element j of accumulator c in group g is pixel pw + 64g + 4j + c (pw = the wave's first
+// pixel): one ds_read_b128 feeds four MFMAs.
+template <int RC, int LAYOUT>
+__device__ __forceinline__ void tile_store(const floatx4 (&acc)[RC][4], float* __restrict__ dst, int64_t P, int k,
+                                           int64_t p0, int q, int r);
+
+template <int RC, int SP, typename T, int LAYOUT, bool NT>
+__global__ void __launch_bounds__(256)
+fit_shared_tile(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P, int64_t lstride,
+                int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  constexpr int R = 256 * RC, S = 4 * SP;
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  const int Npad = (N + S - 1) / S * S;         // whole steps
+  float* __restrict__ lds_pinv = lds_dyn;       // [Npad][16]
+  float* __restrict__ tile = lds_dyn + Npad * 16;  // [2][S][R]
+  for (int idx = threadIdx.x; idx < Npad * 16; idx += 256) {
+    const int n = idx >> 4, i = idx & 15;
+    lds_pinv[idx] = (i < k && n < N) ? pinv[i * N + n] : 0.f;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * R;
+  const T* __restrict__ src = I + (int64_t)blockIdx.y * cstride + t0 + 4 * lane;
+  bool pin[RC];  // this lane's chunk c lies inside the image (P % 4 == 0)
+#pragma unroll
+  for (int c = 0; c < RC; ++c) pin[c] = t0 + 256 * c + 4 * lane < P;
+
+  floatx4 st[SP][RC];
+  auto load_step = [&](int n0) {
+#pragma unroll
+    for (int j = 0; j < SP; ++j) {
+      const int n = n0 + wave * SP + j;
+#pragma unroll
+      for (int c = 0; c < RC; ++c) {
+        float x[4] = {0.f, 0.f, 0.f, 0.f};
+        if (n < N && pin[c]) load_px<T, 4, NT>(src + (int64_t)n * lstride + 256 * c, x);
+        st[j][c] = floatx4{x[0], x[1], x[2], x[3]};
+      }
+    }
+  };
+  auto write_step = [&](int b) {
+    float* __restrict__ tb = tile + b * (S * R);
+#pragma unroll
+    for (int j = 0; j < SP; ++j)
+#pragma unroll
+      for (int c = 0; c < RC; ++c)
+        *reinterpret_cast<floatx4*>(tb + (wave * SP + j) * R + 256 * c + 4 * lane) = st[j][c];
+  };
+  const int q = lane & 15, r = lane >> 4;
+  const int pw = wave * 64 * RC;
+  floatx4 acc[RC][4];
+#pragma unroll
+  for (int g = 0; g < RC; ++g)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[g][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int b, int n0) {
+    const float* __restrict__ tb = tile + b * (S * R);
+#pragma unroll
+    for (int s = 0; s < SP; ++s) {
+      const float a = lds_pinv[(n0 + 4 * s + r) * 16 + q];
+#pragma unroll
+      for (int g = 0; g < RC; ++g) {
+        const floatx4 x = *reinterpret_cast<const floatx4*>(tb + (4 * s + r) * R + pw + 64 * g + 4 * q);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[g][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[c], acc[g][c], 0, 0, 0);
+      }
+    }
+  };
+
+  load_step(0);
+  write_step(0);
+  __syncthreads();
+  int b = 0;
+  for (int n0 = 0; n0 < Npad; n0 += S) {
+    const bool more = n0 + S < Npad;  // workgroup-uniform
+    if (more) load_step(n0 + S);
+    compute(b, n0);
+    if (more) write_step(b ^ 1);  // tile b^1 was last read before the previous barrier
+    __syncthreads();
+    b ^= 1;
+  }
+
+  tile_store<RC, LAYOUT>(acc, coef + (int64_t)blockIdx.y * ocstride, P, k, t0 + pw, q, r);
+}
+
+// DMA form (fp32 stacks): the tile planes go HBM -> LDS by global_load_lds_dwordx4 (no VGPR
+// hop, 1 KiB per wave instruction) into a ring of NB tiles, NB - 1 steps in flight.  A step
+// waits for its own wave's DMAs with a counted vmcnt and one raw s_barrier publishes it to the
+// workgroup (a __syncthreads() would drain every DMA in flight).  Lights past N re-read plane
+// N - 1 (their weights are zero) and lanes past the image re-read its last 4 pixels (never
+// stored), so every DMA is unconditional.
+// one global_load_lds_dwordx4: lane i's 16 bytes land at lds + 16·i (lds wave-uniform)
+template <bool NT>
+__device__ __forceinline__ void glds16(const float* g, float* lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, NT ? 2 : 0);
+}
+
+template <int L, int NB>
+__device__ __forceinline__ void wait_dma(int after) {  // `after` steps of L DMAs issued since
+  if constexpr (NB >= 4) {
+    if (after >= 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * L) : "memory");
+      return;
+    }
+  }
+  if (after >= 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int RC, int SP, int NB, int LAYOUT, bool NT>
+__global__ void __launch_bounds__(256)
+fit_shared_tile_dma(const float* __restrict__ pinv, int k, int N, const float* __restrict__ I, int64_t P,
+                    int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  constexpr int R = 256 * RC, S = 4 * SP, L = SP * RC;
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  const int T = (N + S - 1) / S;  // steps
+  float* __restrict__ lds_pinv = lds_dyn;            // [T·S][16]
+  float* __restrict__ ring = lds_dyn + T * S * 16;  // [NB][S][R]
+  for (int idx = threadIdx.x; idx < T * S * 16; idx += 256) {
+    const int n = idx >> 4, i = idx & 15;
+    lds_pinv[idx] = (i < k && n < N) ? pinv[i * N + n] : 0.f;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * R;
+  const float* __restrict__ src = I + (int64_t)blockIdx.y * cstride;
+  int64_t off[RC];
+#pragma unroll
+  for (int c = 0; c < RC; ++c) {
+    const int64_t px = t0 + 256 * c + 4 * lane;
+    off[c] = px < P ? px : P - 4;
+  }
+  auto issue = [&](int t, int b) {
+    float* rb = ring + b * (S * R);
+#pragma unroll
+    for (int j = 0; j < SP; ++j) {
+      int n = t * S + wave * SP + j;
+      n = n < N ? n : N - 1;
+#pragma unroll
+      for (int c = 0; c < RC; ++c)
+        glds16<NT>(src + (int64_t)n * lstride + off[c], rb + (wave * SP + j) * R + 256 * c);
+    }
+  };
+  const int q = lane & 15, r = lane >> 4;
+  const int pw = wave * 64 * RC;
+  floatx4 acc[RC][4];
+#pragma unroll
+  for (int g = 0; g < RC; ++g)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[g][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // pinv staged; no DMA in flight yet
+#pragma unroll
+  for (int t = 0; t < NB - 1; ++t)
+    if (t < T) issue(t, t);
+  int b = 0;  // ring slot of step t
+  for (int t = 0; t < T; ++t) {
+    wait_dma<L, NB>(min(NB - 2, T - 1 - t));
+    __builtin_amdgcn_s_barrier();
+    const float* __restrict__ tb = ring + b * (S * R);
+#pragma unroll
+    for (int s = 0; s < SP; ++s) {
+      const float a = lds_pinv[(t * S + 4 * s + r) * 16 + q];
+#pragma unroll
+      for (int g = 0; g < RC; ++g) {
+        const floatx4 x = *reinterpret_cast<const floatx4*>(tb + (4 * s + r) * R + pw + 64 * g + 4 * q);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[g][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[c], acc[g][c], 0, 0, 0);
+      }
+    }
+    // slot of step t - 1: every wave has passed this step's barrier, so it is done reading it
+    const int bn = b == 0 ? NB - 1 : b - 1;
+    if (t + NB - 1 < T) issue(t + NB - 1, bn);
+    b = b == NB - 1 ? 0 : b + 1;
+  }
+  tile_store<RC, LAYOUT>(acc, coef + (int64_t)blockIdx.y * ocstride, P, k, t0 + pw, q, r);
+}
+
+// acc[g][c][rr] = coefficient 4r + rr of pixel p0 + 64g + 4q + c (p0 = the wave's first pixel)
+template <int RC, int LAYOUT>
+__device__ __forceinline__ void tile_store(const floatx4 (&acc)[RC][4], float* __restrict__ dst, int64_t P, int k,
+                                           int64_t p0, int q, int r) {
+#pragma unroll
+  for (int g = 0; g < RC; ++g) {
+    const int64_t px = p0 + 64 * g + 4 * q;
+    if (px >= P) continue;
+    if constexpr (LAYOUT == RTI_COEF_PLANAR) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = 4 * r + rr;
+        if (i < k)
+          *reinterpret_cast<floatx4*>(dst + (int64_t)i * P + px) =
+              floatx4{acc[g][0][rr], acc[g][1][rr], acc[g][2][rr], acc[g][3][rr]};
+      }
+    } else if (k == 16) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *reinterpret_cast<floatx4*>(dst + (px + c) * 16 + 4 * r) = acc[g][c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          if (4 * r + rr < k) dst[(px + c) * k + 4 * r + rr] = acc[g][c][rr];
+    }
+  }
+}
+
 struct FitArgs {
   const float* pinv;
   int k, N;
@@ -463,6 +680,87 @@ void launch_mfma(const FitArgs& a) {
   }
 }
 
+template <int RC, int SP, typename T, int LAYOUT, bool NT>
+int launch_tile_t(const FitArgs& a) {
+  constexpr int R = 256 * RC, S = 4 * SP;
+  const int Npad = (a.N + S - 1) / S * S;
+  const size_t lds = ((size_t)Npad * 16 + (size_t)2 * S * R) * sizeof(float);
+  if (lds > 160 * 1024)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
+  auto kern = fit_shared_tile<RC, SP, T, LAYOUT, NT>;
+  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
+  dim3 grid(grid_1d(a.P, R), a.C);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, a.stream, a.pinv, a.k, a.N, static_cast<const T*>(a.I), a.P,
+                     a.lstride, a.cstride, a.coef, a.ocstride);
+  return RTI_OK;
+}
+
+template <int RC, int SP, typename T>
+int launch_tile_l(const FitArgs& a) {
+  if (a.layout == RTI_COEF_PLANAR)
+    return a.nt ? launch_tile_t<RC, SP, T, RTI_COEF_PLANAR, true>(a) : launch_tile_t<RC, SP, T, RTI_COEF_PLANAR, false>(a);
+  return a.nt ? launch_tile_t<RC, SP, T, RTI_COEF_PIXEL_MAJOR, true>(a)
+              : launch_tile_t<RC, SP, T, RTI_COEF_PIXEL_MAJOR, false>(a);
+}
+
+template <int RC, int SP, int NB, int LAYOUT, bool NT>
+int launch_tile_dma_t(const FitArgs& a) {
+  constexpr int R = 256 * RC, S = 4 * SP;
+  const int Npad = (a.N + S - 1) / S * S;
+  const size_t lds = ((size_t)Npad * 16 + (size_t)NB * S * R) * sizeof(float);
+  if (lds > 160 * 1024)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile ring of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
+  auto kern = fit_shared_tile_dma<RC, SP, NB, LAYOUT, NT>;
+  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
+  dim3 grid(grid_1d(a.P, R), a.C);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, a.stream, a.pinv, a.k, a.N, static_cast<const float*>(a.I), a.P,
+                     a.lstride, a.cstride, a.coef, a.ocstride);
+  return RTI_OK;
+}
+
+template <int RC, int SP, int NB>
+int launch_tile_dma_l(const FitArgs& a) {
+  if (a.layout == RTI_COEF_PLANAR)
+    return a.nt ? launch_tile_dma_t<RC, SP, NB, RTI_COEF_PLANAR, true>(a)
+                : launch_tile_dma_t<RC, SP, NB, RTI_COEF_PLANAR, false>(a);
+  return a.nt ? launch_tile_dma_t<RC, SP, NB, RTI_COEF_PIXEL_MAJOR, true>(a)
+              : launch_tile_dma_t<RC, SP, NB, RTI_COEF_PIXEL_MAJOR, false>(a);
+}
+
+template <int NB>
+int launch_tile_dma(const FitArgs& a, int rc, int sp) {
+  if (sp >= 2) return rc >= 4 ? launch_tile_dma_l<4, 2, NB>(a) : launch_tile_dma_l<2, 2, NB>(a);
+  return rc >= 8 ? launch_tile_dma_l<8, 1, NB>(a) : launch_tile_dma_l<4, 1, NB>(a);
+}
+
+// rc: 1 KiB chunks per wave and plane (tile = 256·rc pixels), sp: planes per wave and step,
+// depth: tiles in the LDS ring (2 = register-staged double buffer; 3, 4 = DMA ring, fp32 only).
+// Every (rc, sp) for fp32 stacks; 8-bit and int32 stacks use the register-staged (4, 1).
+template <typename T>
+int launch_tile(const FitArgs& a, int rc, int sp, int depth) {
+  if constexpr (std::is_same<T, float>::value) {
+    if (depth >= 4) return launch_tile_dma<4>(a, rc, sp);
+    if (depth == 3) return launch_tile_dma<3>(a, rc, sp);
+  }
+  if (!std::is_same<T, float>::value || (rc == 4 && sp <= 1)) return launch_tile_l<4, 1, T>(a);
+  if constexpr (std::is_same<T, float>::value) {
+    if (sp >= 2) {
+      if (rc >= 8) return launch_tile_l<8, 2, T>(a);
+      if (rc >= 4) return launch_tile_l<4, 2, T>(a);
+      if (rc >= 2) return launch_tile_l<2, 2, T>(a);
+      return launch_tile_l<1, 2, T>(a);
+    }
+    if (rc >= 8) return launch_tile_l<8, 1, T>(a);
+    if (rc >= 2) return launch_tile_l<2, 1, T>(a);
+    return launch_tile_l<1, 1, T>(a);
+  }
+  return RTI_OK;
+}
+
 size_t dtype_size(int dt) {
   switch (dt) {
     case RTI_F32: return 4;
@@ -523,7 +821,7 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
   bool use_mfma;
   if (sel == RTI_KERNEL_MFMA) {
     use_mfma = true;
-  } else if (sel == RTI_KERNEL_VALU) {
+  } else if (sel == RTI_KERNEL_VALU || sel == RTI_KERNEL_TILE) {
     use_mfma = false;
   } else {
     // AUTO: measured best on MI355X (profiles/): the VALU stream with
@@ -553,6 +851,28 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
   }
   const bool mfma_ok = N <= 1024 && P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 &&
                        aligned_to(I, 4 * es) && aligned_to(coef, 16) && a.ocstride % 4 == 0;
+  // AUTO for HSH-16 on fp32 stacks: the LDS-tiled MFMA kernel (c4 4K RGB x 200: 3.54 vs 3.73 ms
+  // and 3.94 vs 4.20 ms on two boxes, profiles/r01_c4_tile_sweep.log), when the image gives at
+  // least 1024 tiles of 2048 pixels; PTM-6 stays on the VALU stream (c3: 0.54 vs 0.62 ms).
+  const bool auto_tile = sel == RTI_KERNEL_AUTO && k == 16 && in_dtype == RTI_F32 && P * C >= (int64_t)1024 * 2048;
+  if (sel == RTI_KERNEL_TILE || (auto_tile && mfma_ok)) {
+    if (mfma_ok) {
+      // default tile: 2048 pixels x 8 planes per step, register-staged (1024 pixels above N = 512,
+      // where the 128 KiB double tile and the [N][16] pseudo-inverse no longer fit 160 KiB of LDS)
+      const int rc = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, sp = (kernel >> RTI_KERNEL_TILE_PLANES_SHIFT) & 0xF;
+      const int depth = (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF;
+      const int rc0 = rc ? rc : (N <= 512 ? 8 : 4);
+      int st;
+      switch (in_dtype) {
+        case RTI_F32: st = launch_tile<float>(a, rc0, sp ? sp : 2, depth ? depth : 2); break;
+        case RTI_I32: st = launch_tile<int32_t>(a, 4, 1, 2); break;
+        default: st = launch_tile<uint8_t>(a, 4, 1, 2); break;
+      }
+      return st != RTI_OK ? st : check_launch("rti_fit_shared");
+    }
+    if (!valu_k) return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: tile path needs N<=1024 and 4-pixel alignment");
+    a.nc = 1;  // ragged shapes: the one-chunk VALU stream
+  }
   if (use_mfma && !mfma_ok) {
     if (sel == RTI_KERNEL_MFMA && !valu_k)
       return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: MFMA path needs N<=1024 and 4-pixel alignment");

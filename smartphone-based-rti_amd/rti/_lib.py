@@ -38,11 +38,14 @@ RTI_OUT_PIXEL_MAJOR = 1
 RTI_KERNEL_AUTO = 0
 RTI_KERNEL_VALU = 1
 RTI_KERNEL_MFMA = 2
+RTI_KERNEL_TILE = 3
 RTI_KERNEL_NONTEMPORAL = 0x100
 RTI_KERNEL_PINV_LDS = 0x200
 RTI_KERNEL_NT_STORE = 0x400
 RTI_KERNEL_STAGE = 0x800
 RTI_KERNEL_CHUNKS_SHIFT = 12  # VALU chunks per lane in bits 12-15 (0 = AUTO)
+RTI_KERNEL_TILE_PLANES_SHIFT = 16  # TILE kernel: light planes per wave and step in bits 16-19 (0 = 2)
+RTI_KERNEL_TILE_DEPTH_SHIFT = 20  # TILE kernel: tiles in the LDS ring in bits 20-23 (0 = 2)
 
 
 class RTILibraryMissing(ImportError):

@@ -27,7 +27,7 @@ BASES = {
     "hsh": L.RTI_BASIS_HSH16, "hsh3": L.RTI_BASIS_HSH16, "hsh16": L.RTI_BASIS_HSH16,
     "hsh2": L.RTI_BASIS_HSH9, "hsh9": L.RTI_BASIS_HSH9,
 }
-_KERNELS = {"auto": L.RTI_KERNEL_AUTO, "valu": L.RTI_KERNEL_VALU, "mfma": L.RTI_KERNEL_MFMA}
+_KERNELS = {"auto": L.RTI_KERNEL_AUTO, "valu": L.RTI_KERNEL_VALU, "mfma": L.RTI_KERNEL_MFMA, "tile": L.RTI_KERNEL_TILE}
 _IN_DTYPES = {torch.float32: L.RTI_F32, torch.uint8: L.RTI_U8, torch.int32: L.RTI_I32}
 _COEF_DTYPES = {torch.float32: L.RTI_F32, torch.float64: L.RTI_F64}
 _OUT_DTYPES = {torch.float32: L.RTI_F32, torch.float64: L.RTI_F64, torch.int32: L.RTI_I32, torch.uint8: L.RTI_U8}

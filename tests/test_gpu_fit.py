@@ -11,7 +11,7 @@ from conftest import coef_close, golden
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["valu", "mfma"]
+KERNELS = ["valu", "mfma", "tile"]
 
 
 def to_dev(a, dev, dtype=torch.float32):
@@ -162,6 +162,57 @@ def test_full_size_4k_n100_properties(cuda, kernel):
     coef2 = rti.fit((2 * I + 3).reshape(N, H, W), lu, lv, kernel=kernel, layout="planar").reshape(6, -1)
     c3 = torch.as_tensor(o.pinv_shared("ptm", lu, lv).sum(1) * 3, device=cuda, dtype=torch.float32)[:, None]
     assert float(((coef2 - 2 * coef - c3).abs() / (2 * scale)).max()) < 1e-4
+
+
+@pytest.mark.parametrize("layout", ["pixel", "planar"])
+def test_auto_hsh_large_image(cuda, layout):
+    """AUTO on an HSH-16 fp32 stack big enough for the LDS-tiled MFMA kernel (>= 1024 tiles):
+    2 channels x 1100 x 1000 px x 23 lights (a partial tile and a partial light step), sampled
+    pixels against the fp64 oracle."""
+    C, H, W, N = 2, 1100, 1000, 23
+    lu, lv = o.synth_dirs(N, 5)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    I = torch.randint(0, 256, (C, N, H, W), generator=g, device=cuda).float()
+    coef = rti.fit(I, lu, lv, basis="hsh", layout=layout)
+    pinv64 = np.linalg.pinv(o.design("hsh", lu, lv))
+    idx = torch.randint(0, H * W, (4096,), generator=g, device=cuda)
+    for c in range(C):
+        ref = (pinv64 @ I[c].reshape(N, -1)[:, idx].cpu().numpy().astype(np.float64)).T
+        got = coef[c].reshape(H * W, 16)[idx] if layout == "pixel" else coef[c].reshape(16, H * W)[:, idx].T
+        err, ok = coef_close(got.cpu().numpy(), ref)
+        assert ok, (c, err)
+
+
+@pytest.mark.parametrize("rc,sp", [(1, 1), (2, 1), (4, 1), (8, 1), (1, 2), (2, 2), (4, 2), (8, 2)])
+@pytest.mark.parametrize("basis,n", [("hsh", 29), ("hsh9", 10), ("ptm", 37), ("hsh9", 200)])
+@pytest.mark.parametrize("nt", [0, 0x100])
+@pytest.mark.parametrize("depth", [2, 3, 4])
+def test_lds_tile_variants(cuda, rc, sp, basis, n, nt, depth):
+    """MFMA kernel on the LDS tile (RTI_KERNEL_TILE): tile widths 256·rc, 4·sp planes per step with
+    light counts that leave a partial last step, register-staged (depth 2) and DMA-ring (3, 4)
+    staging, pixel counts around tile multiples (partial tiles, lanes past the image), two
+    channels, both coefficient layouts."""
+    k = rti.basis_terms(basis)
+    lu, lv = o.synth_dirs(n, 17)
+    pinv64 = np.linalg.pinv(o.design("hsh" if basis != "ptm" else "ptm", lu, lv)[:, :k])
+    pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=cuda)
+    R = 256 * rc
+    flags = nt | (rc << rti._lib.RTI_KERNEL_CHUNKS_SHIFT) | (sp << rti._lib.RTI_KERNEL_TILE_PLANES_SHIFT) | \
+        (depth << rti._lib.RTI_KERNEL_TILE_DEPTH_SHIFT)
+    for P in (4, R - 4, R, R + 4, 3 * R + 260):
+        rng = np.random.default_rng(P + n)
+        I = rng.integers(0, 256, size=(2, n, P)).astype(np.float32)
+        ref = np.einsum("kn,cnp->cpk", pinv64, I.astype(np.float64))
+        for layout in ("pixel", "planar"):
+            coef = torch.full((2, P, k) if layout == "pixel" else (2, k, P), float("nan"), device=cuda)
+            rti.fit_shared_into(pv, torch.as_tensor(I, device=cuda), coef, k=k, layout=layout, kernel="tile",
+                                flags=flags)
+            got = coef.cpu().numpy()
+            if layout == "planar":
+                got = np.moveaxis(got, 1, 2)
+            for c in range(2):
+                err, ok = coef_close(got[c], ref[c])
+                assert ok, (P, layout, c, err)
 
 
 @pytest.mark.parametrize("chunks", [1, 2, 3, 4, 8])

@@ -51,6 +51,10 @@ def main():
         for o in opts:  # c<n>: chunks per lane (rti.h RTI_KERNEL_CHUNKS)
             if o[:1] == "c" and o[1:].isdigit():
                 fl |= int(o[1:]) << 12
+            if o[:1] == "t" and o[1:].isdigit():  # t<sp>: TILE kernel planes per wave and step
+                fl |= int(o[1:]) << 16
+            if o[:1] == "d" and o[1:].isdigit():  # d<n>: TILE kernel LDS ring depth
+                fl |= int(o[1:]) << 20
         variants.append((v, parts[0], parts[1], fl))
     probe = None
     plib = os.path.join(ROOT, "tools", "probe", "libhbm_probe.so")
