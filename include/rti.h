@@ -119,6 +119,21 @@ int rti_fit_shared(const float* pinv, int k, int N,
                    float* coef, int coef_layout, int64_t coef_channel_stride,
                    int kernel, rti_stream_t stream);
 
+/* ---- device: per-pixel residuals of the shared-direction fit -----------------------
+ * Fit quality next to rti_fit_shared's coefficients (the reference computes the same
+ * least-squares solution, analysis.py:280-298, and never reports its residual):
+ *   res[c][p]     = sqrt( Σ_n (I[c][n][p] − Σ_i A[n][i]·coef[c][p][i])² / N )
+ *   partial[c][b] = Σ of the squared residuals (before /N) of workgroup b's pixels, fp64
+ * A: device fp32 design matrix [N][k] (rti_design_matrix rounded to fp32); k ∈ {6, 9, 16}.
+ * I / coef / strides exactly as rti_fit_shared.  res: device fp32 [C][P].
+ * partial: NULL, or device fp64 [C][rti_fit_residual_blocks(P)] that the caller zeroes
+ * (entries past the launched grid stay 0); its sum over b is channel c's residual energy.
+ * A second HBM pass over the stack (4 + 4(k+1)/N bytes per pixel·light). */
+int64_t rti_fit_residual_blocks(int64_t P);
+int rti_fit_residual(const float* A, int k, int N, const void* I, int in_dtype, int64_t P, int C,
+                     int64_t light_stride, int64_t channel_stride, const float* coef, int coef_layout,
+                     int64_t coef_channel_stride, float* res, double* partial, rti_stream_t stream);
+
 /* ---- device: per-pixel PTM fit, light vectors generated in-kernel ------------------
  * Fuses compute_intensities' light vectors (analysis.py:221-231) into the
  * per-pixel PTM solve (analysis.py:280-298): for pixel (x, y) of an H×W stack

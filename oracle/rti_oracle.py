@@ -284,6 +284,17 @@ def fit_shared_f32(I_np, pinv):
     return (np.asarray(pinv, np.float32) @ I2).T
 
 
+def fit_residual(I_np, A, coef):
+    """Per-pixel RMS residual of a shared fit and the residual energy (test oracle of
+    rti_fit_residual; the reference solves the same least squares, analysis.py:280-298,
+    but never reports the residual).  I_np: [N, P] light-major; A: [N, k]; coef: [P, k].
+    Returns (res[P] = sqrt(Σ_n r² / N), ss_total = Σ_p Σ_n r²), fp64."""
+    I2 = np.asarray(I_np, np.float64).reshape(I_np.shape[0], -1)
+    r = I2 - np.asarray(A, np.float64) @ np.asarray(coef, np.float64).reshape(I2.shape[1], -1).T
+    ss = (r * r).sum(axis=0)
+    return np.sqrt(ss / I2.shape[0]), float(ss.sum())
+
+
 def fit_perpixel(lu, lv, inten, basis="ptm"):
     """Per-pixel fit with each pixel's own (lu, lv) list (analysis.py:350-359).
 

@@ -226,6 +226,48 @@ def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=Non
     return coef
 
 
+def fit_residual(I, coef, lu, lv, basis="ptm", *, layout="pixel"):
+    """Per-pixel RMS residual of a shared-direction fit (``rti_fit_residual``).
+
+    I: the stack ``fit`` was given ([N, P], [N, H, W] or [C, N, H, W]); coef: its
+    fp32 output (same layout).  Returns ``(res, rms)``: res fp32 with I's spatial
+    shape (plus the leading C for 4-D stacks) = sqrt(Σ_n (I_n − A_n·coef)² / N), and
+    rms fp64 [C] (or a 0-d tensor) = the RMS residual over all pixels of a channel,
+    summed from per-workgroup wavefront reductions on the device."""
+    _require_cuda(I, "I")
+    _require_cuda(coef, "coef")
+    cl = _layout_id(layout)
+    b = basis_id(basis)
+    k = basis_terms(b)
+    if I.dim() == 2:
+        (N, P), C, spatial = I.shape, 1, (I.shape[1],)
+    elif I.dim() == 3:
+        N, H, W = I.shape
+        C, P, spatial = 1, H * W, (H, W)
+    elif I.dim() == 4:
+        C, N, H, W = I.shape
+        P, spatial = H * W, (H, W)
+    else:
+        raise ValueError("I must be [N, P], [N, H, W] or [C, N, H, W]")
+    if coef.dtype != torch.float32 or coef.numel() != C * P * k:
+        raise ValueError(f"coef must be fp32 with {C}x{P}x{k} elements (the output of fit)")
+    A = design_matrix(lu, lv, b)
+    if A.shape[0] != N:
+        raise ValueError(f"{A.shape[0]} light directions for {N} intensity planes")
+    A_dev = torch.as_tensor(A.astype(np.float32), device=I.device).contiguous()
+    Ic = I.contiguous().reshape(C, N, P)
+    cc = coef.contiguous()
+    res = torch.empty((C, P), dtype=torch.float32, device=I.device)
+    nb = int(L.lib().rti_fit_residual_blocks(P))
+    partial = torch.zeros((C, nb), dtype=torch.float64, device=I.device)
+    st = L.lib().rti_fit_residual(_vp(A_dev), k, N, _vp(Ic), _IN_DTYPES[Ic.dtype], P, C, P, N * P, _vp(cc), cl,
+                                  P * k, _vp(res), _vp(partial), _stream_of(I))
+    L.check(st, "rti_fit_residual")
+    rms = torch.sqrt(partial.sum(dim=1) / (P * N))
+    res = res.reshape((C,) + spatial)
+    return (res, rms) if I.dim() == 4 else (res[0], rms[0])
+
+
 def light_dirs(cams, H, W, origin=(0.0, 0.0), device="cuda"):
     """compute_intensities' light vectors on the GPU: (lu, lv) fp32 [H, W, N]."""
     cams_d = torch.as_tensor(np.asarray(cams.detach().cpu() if torch.is_tensor(cams) else cams, np.float64),

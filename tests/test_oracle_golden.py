@@ -142,3 +142,19 @@ def test_hsv2bgr_known_answers():
     # V substitution + clip as relighting_event does (interactive_relighting.py:33-38)
     img = o.relighting_event_image(np.array([[300, -4]], np.int32), np.array([[[0, 0, 9], [0, 0, 9]]], np.uint8))
     assert np.array_equal(img, np.array([[[255] * 3, [0] * 3]], np.uint8))
+
+
+def test_fit_residual_oracle_identity():
+    """The residual restatement against the normal-equation identity
+    ‖I − A c‖² = ‖I‖² − cᵀAᵀI (exact for the least-squares c), in fp64 on the golden stack."""
+    d = golden("ptm_shared_256x256_N20.npz")
+    I = np.asarray(d["I"], np.float64).reshape(d["I"].shape[0], -1)
+    A = o.design("ptm", d["lu"], d["lv"])
+    coef = o.fit_shared(I, o.pinv_shared("ptm", d["lu"], d["lv"]))
+    res, ss = o.fit_residual(I, A, coef)
+    ident = (I * I).sum(0) - np.einsum("pk,nk,np->p", coef, A, I)
+    np.testing.assert_allclose(res * res * I.shape[0], ident, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(ss, ident.sum(), rtol=1e-9)
+    # the reference's golden coefficients explain the stack equally well
+    res_g, _ = o.fit_residual(I, A, np.asarray(d["coef"]).reshape(-1, 6))
+    np.testing.assert_allclose(res_g, res, rtol=1e-6, atol=1e-9)
