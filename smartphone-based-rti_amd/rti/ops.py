@@ -1,4 +1,4 @@
-"""PyTorch custom ops over the C ABI: ``torch.ops.rti.fit_shared`` / ``torch.ops.rti.relight``.
+"""PyTorch custom ops over the C ABI: ``torch.ops.rti.fit_shared`` / ``fit_residual`` / ``relight``.
 
 They let the fit and relight kernels sit inside torch programs (and
 ``torch.library`` fake-tensor tracing) while the compute stays in librti's
@@ -38,6 +38,35 @@ def _(pinv, I, planar=False, kernel=0):
     if I.dim() == 3:
         shape = (I.shape[0],) + shape
     return I.new_empty(shape, dtype=torch.float32)
+
+
+@torch.library.custom_op("rti::fit_residual", mutates_args=())
+def fit_residual(A: torch.Tensor, I: torch.Tensor, coef: torch.Tensor) -> torch.Tensor:
+    """Per-pixel RMS residual of coef (fp32 [P, k], fit_shared's pixel-major output) against
+    I (CUDA [N, P]) under the fp32 design matrix A [N, k] -> fp32 [P]."""
+    api._require_cuda(I, "I")
+    api._require_cuda(A, "A")
+    api._require_cuda(coef, "coef")
+    if A.dtype != torch.float32 or coef.dtype != torch.float32:
+        raise ValueError("A and coef must be float32")
+    if I.dim() != 2:
+        raise ValueError("I must be [N, P]")
+    N, P = I.shape
+    k = A.shape[1]
+    if A.shape[0] != N or coef.shape != (P, k):
+        raise ValueError(f"A must be [{N}, k] and coef [{P}, k]")
+    Ic, Ac, cc = I.contiguous(), A.contiguous(), coef.contiguous()
+    res = torch.empty(P, dtype=torch.float32, device=I.device)
+    st = L.lib().rti_fit_residual(api._vp(Ac), k, N, api._vp(Ic), api._IN_DTYPES[Ic.dtype], P, 1, P, N * P,
+                                  api._vp(cc), L.RTI_COEF_PIXEL_MAJOR, P * k, api._vp(res), None,
+                                  api._stream_of(I))
+    L.check(st, "rti_fit_residual")
+    return res
+
+
+@fit_residual.register_fake
+def _(A, I, coef):
+    return I.new_empty((I.shape[-1],), dtype=torch.float32)
 
 
 @torch.library.custom_op("rti::relight", mutates_args=())

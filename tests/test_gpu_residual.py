@@ -114,3 +114,15 @@ def test_full_size_4k_n100(cuda):
     assert abs(float(rms) ** 2 - mean_sq) <= 1e-6 * mean_sq
     expect = 2.0 * np.sqrt((n - 6) / n)
     assert abs(float(rms) - expect) < 0.01 * expect
+
+
+def test_custom_op_matches_api(cuda):
+    from rti import ops  # noqa: F401  registers torch.ops.rti.*
+    d = golden("ptm_shared_256x256_N20.npz")
+    I = torch.as_tensor(d["I"]).to(cuda).to(torch.float32)
+    coef = rti.fit(I, d["lu"], d["lv"])
+    res, _ = rti.fit_residual(I, coef, d["lu"], d["lv"])
+    A = torch.as_tensor(rti.design_matrix(d["lu"], d["lv"]).astype(np.float32), device=cuda)
+    N = I.shape[0]
+    got = torch.ops.rti.fit_residual(A, I.reshape(N, -1), coef.reshape(-1, 6))
+    assert torch.equal(got, res.reshape(-1))
