@@ -46,7 +46,10 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-template <int K, int VEC, typename T>
+// Wide lanes (as the fit): a wave owns NC·64·VEC consecutive pixels and
+// lane l's chunk j is the VEC pixels at wave_base + j·64·VEC + VEC·l, so the wave's NC loads
+// of one light plane cover NC KiB contiguous (VEC = 4, fp32).
+template <int K, int VEC, int NC, typename T>
 __global__ __launch_bounds__(RES_THREADS) void fit_residual_k(const float* __restrict__ A, int N,
                                                              const T* __restrict__ I, int64_t P,
                                                              int64_t lstride, int64_t cstride,
@@ -54,48 +57,63 @@ __global__ __launch_bounds__(RES_THREADS) void fit_residual_k(const float* __res
                                                              int64_t ocstride, float* __restrict__ res,
                                                              double* __restrict__ partial, int64_t pstride) {
   const int c = blockIdx.y;
-  const int64_t p0 = ((int64_t)blockIdx.x * RES_THREADS + threadIdx.x) * VEC;
+  const int64_t wave = ((int64_t)blockIdx.x * RES_THREADS + threadIdx.x) >> 6;
+  const int64_t base = wave * (NC * 64 * VEC) + (threadIdx.x & 63) * VEC;
   const T* Ic = I + c * cstride;
   const float* cc = coef + c * ocstride;
   double mine = 0.0;
-  if (p0 < P) {
-    float a[VEC][K];
+  bool live[NC];
+  float a[NC][VEC][K];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int64_t p0 = base + j * 64 * VEC;
+    live[j] = p0 < P;
+    if (!live[j]) continue;
     if (layout == RTI_COEF_PIXEL_MAJOR) {
 #pragma unroll
       for (int v = 0; v < VEC; ++v)
 #pragma unroll
-        for (int i = 0; i < K; ++i) a[v][i] = cc[(p0 + v) * K + i];
+        for (int i = 0; i < K; ++i) a[j][v][i] = cc[(p0 + v) * K + i];
     } else {
 #pragma unroll
       for (int i = 0; i < K; ++i) {
         float x[VEC];
         load_vec<float, VEC>(cc + i * P + p0, x);
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) a[v][i] = x[v];
+        for (int v = 0; v < VEC; ++v) a[j][v][i] = x[v];
       }
     }
-    float ss[VEC] = {};
-    for (int n = 0; n < N; ++n) {
-      float x[VEC];
-      load_vec<T, VEC>(Ic + n * lstride + p0, x);
-      const float* An = A + (int64_t)n * K;  // wave-uniform row
+  }
+  float ss[NC][VEC] = {};
+  for (int n = 0; n < N; ++n) {
+    float x[NC][VEC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+      if (live[j]) load_vec<T, VEC>(Ic + n * lstride + base + j * 64 * VEC, x[j]);
+    const float* An = A + (int64_t)n * K;  // wave-uniform row
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
         float pred = 0.f;
 #pragma unroll
-        for (int i = 0; i < K; ++i) pred = fmaf(An[i], a[v][i], pred);
-        const float r = x[v] - pred;
-        ss[v] = fmaf(r, r, ss[v]);
+        for (int i = 0; i < K; ++i) pred = fmaf(An[i], a[j][v][i], pred);
+        const float r = x[j][v] - pred;
+        ss[j][v] = fmaf(r, r, ss[j][v]);
       }
     }
+  }
+  const float invN = 1.0f / (float)N;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    if (!live[j]) continue;
     float out[VEC];
-    const float invN = 1.0f / (float)N;
 #pragma unroll
     for (int v = 0; v < VEC; ++v) {
-      out[v] = sqrtf(ss[v] * invN);
-      mine += (double)ss[v];
+      out[v] = sqrtf(ss[j][v] * invN);
+      mine += (double)ss[j][v];
     }
-    float* rc = res + c * P + p0;
+    float* rc = res + c * P + base + j * 64 * VEC;
     if constexpr (VEC == 4) {
       *reinterpret_cast<float4*>(rc) = make_float4(out[0], out[1], out[2], out[3]);
     } else {
@@ -131,18 +149,23 @@ struct ResArgs {
   hipStream_t s;
 };
 
-template <int K, int VEC, typename T>
+template <int K, int VEC, int NC, typename T>
 int launch_res(const ResArgs& a) {
-  const dim3 grid(grid_1d(a.P, RES_THREADS * VEC), a.C);
-  hipLaunchKernelGGL((fit_residual_k<K, VEC, T>), grid, dim3(RES_THREADS), 0, a.s, a.A, a.N,
+  const dim3 grid(grid_1d(a.P, RES_THREADS * VEC * NC), a.C);
+  hipLaunchKernelGGL((fit_residual_k<K, VEC, NC, T>), grid, dim3(RES_THREADS), 0, a.s, a.A, a.N,
                      static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.layout, a.ocstride, a.res,
                      a.partial, (int64_t)grid_1d(a.P, RES_THREADS));
   return check_launch("rti_fit_residual");
 }
 
+// Chunks per lane, measured at 4K x 100 (profiles/r01_residual_c3_nc_sweep.log): PTM-6
+// NC = 1 / 2 / 4 / 8 -> 0.522 / 0.520 / 0.505 / 0.578 ms (8 chunks = 256 VGPRs, 1 wave/SIMD,
+// cannot hide the coefficient loads).  HSH-9/16 keep one chunk (wide lanes not measured).
 template <int K, typename T>
 int launch_res_v(const ResArgs& a, bool vec4) {
-  return vec4 ? launch_res<K, 4, T>(a) : launch_res<K, 1, T>(a);
+  if (!vec4) return launch_res<K, 1, 1, T>(a);
+  if (K == 6 && a.P * a.C / (64 * 4 * 4) >= 2000) return launch_res<K, 4, (K == 6 ? 4 : 1), T>(a);
+  return launch_res<K, 4, 1, T>(a);
 }
 
 template <typename T>

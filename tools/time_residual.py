@@ -45,7 +45,7 @@ def main(steps=20, warmup=5):
     ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
     alg = 4.0 * P * n + 4.0 * P * k + 4.0 * P
     gbs = alg / (ms * 1e-3) / 1e9
-    print(json.dumps({"kernel": "fit_residual_k<6,4,float>", "config": "3840x2160 N=100 PTM-6 fp32",
+    print(json.dumps({"kernel": "fit_residual_k<6,4,4,float>", "config": "3840x2160 N=100 PTM-6 fp32",
                       "median_ms": round(ms, 4), "alg_bytes": alg, "achieved_GBs": round(gbs, 1),
                       "frac_of_8TBs": round(gbs / 8000.0, 4)}))
 
