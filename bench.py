@@ -1,24 +1,35 @@
 #!/usr/bin/env python3
-"""Benchmark of the shared-direction PTM fit (BASELINE.json metric).
+"""Benchmark of the shared-direction PTM fit (BASELINE.json metric) and the other §8 rows.
 
-Metric: Mpix·lights/s of the 6-coefficient PTM fit on a 3840×2160 × 100-light
-fp32 stack (BASELINE.json configs[2], the metric's config; it fits one GPU).
-One step = one rti_fit_shared launch over the whole stack, inputs resident in
-HBM.  With --gpus N (launched by torch.distributed.run) every rank fits its own
-2160-row stripe of a G·2160-row image (row-tiled shards, weak scaling) with no
-collective in the timed region; --allgather adds the RCCL all-gather that
-reassembles the coefficient maps and reports it separately.
+Metric: Mpix·lights/s of the 6-coefficient PTM fit on a 3840×2160 × 100-light fp32 stack
+(BASELINE.json configs[2], "at 1/2/4/8 GPU").  One step = one rti_fit_shared launch per rank
+over that rank's row block, inputs resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--kernel auto]
+Multi-GPU: one process per GPU.  ``--gpus N`` without WORLD_SIZE in the
+environment re-launches this script under ``torch.distributed.run`` with N ranks (before the
+parent touches the GPU); the driver's own torchrun launch is used as is.  Default = STRONG
+scaling: rank r fits rows row_range(H, G, r) (2160/G rows of the same 4K image) with the
+replicated k×N pseudo-inverse and no collective in the timed region; value = all pixel·lights of
+the image ÷ the max-over-ranks time.  ``--weak`` gives every rank a whole H-row image instead.
+The RCCL all-gather that reassembles the maps (the north_star's only collective) is timed
+separately (``allgather_ms``), and so is the row-chunked fit with each chunk's all-gather
+overlapped with the next chunk's fit (``fit_allgather_overlapped_ms``).
 
-Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1) is the oracle's
-NumPy restatement (fp64 pinv + fp32 matmul) timed on a bounded sample.
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--weak]
+
+Rank 0 prints one JSON line.  It carries ``roofline`` (kernel time = median of 50 HIP-event
+pairs after 10 warm-ups on the launch stream), an in-run ``parity`` check of sampled outputs
+against the CPU oracle (BASELINE.md plan step 5) and ``cpu_baseline`` (rank 0, N = 1: the
+oracle's NumPy restatement on a bounded sample, at the affinity thread count and at 1 thread).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,10 +37,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "smartphone-based-rti_amd"))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TFLOPS = 78.6
 
 CONFIGS = {
     # name: (kind, H, W, lights/evals, channels, basis, description)
@@ -43,15 +54,58 @@ CONFIGS = {
     "c7": ("operator", 400, 400, 100, 1, "rbf",
            "linear-RBF interpolation (reference default, SciPy Rbf) of a 400x400 ROI x 100 shared lights on the "
            "100x100 grid -> int32 tables (interpolate_intensities + prepare_images_data)"),
-    "c9": ("frame", 2160, 3840, 1000, 1, "ptm",
-           "interactive relight frame 3840x2160 (relighting_event): PTM-6 maps at one cursor (lu,lv) -> int32 -> "
-           "clip -> V of the HSV ROI -> OpenCV HSV2BGR, one launch per event"),
     "c8": ("rbf_perpixel", 400, 400, 100, 1, "rbf",
            "reference default pipeline: per-pixel linear RBF (own light list per pixel, fp64 LU) of a 400x400 ROI x "
            "100 lights on the 100x100 grid -> int32 tables"),
+    "c8n200": ("rbf_perpixel", 400, 400, 200, 1, "rbf",
+               "reference default pipeline at N=200 (SURVEY §6): per-pixel linear RBF of a 400x400 ROI x 200 lights "
+               "on the 100x100 grid -> int32 tables"),
+    "c9": ("frame", 2160, 3840, 1000, 1, "ptm",
+           "interactive relight frame 3840x2160 (relighting_event): PTM-6 maps at one cursor (lu,lv) -> int32 -> "
+           "clip -> V of the HSV ROI -> OpenCV HSV2BGR, one launch per event"),
+    "c10": ("fit_residual", 2160, 3840, 100, 1, "ptm",
+            "ptm6-fit + per-pixel residuals in ONE pass, 3840x2160 N=100 fp32 (north_star residuals)"),
 }
-MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+DEFAULT_STEPS = {"fit": 20, "fit_residual": 20, "relight": 1000, "frame": 1000, "perpixel": 10, "operator": 10,
+                 "rbf_perpixel": 3}
 
+
+# ---- launcher ---------------------------------------------------------------------------------
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def maybe_spawn(args):
+    """--gpus N > 1 outside a torchrun launch: start N fresh ranks under torch.distributed.run and
+    exit with their status.  Runs before anything in this process touches the GPU."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.run(cmd, env=env).returncode)
+
+
+class Ctx:
+    """This rank's share of the image: rows [r0, r1) of an H-row image."""
+
+    def __init__(self, args, H, rank, world, dev):
+        from rti.parallel import row_range
+
+        self.rank, self.world, self.dev, self.weak = rank, world, dev, args.weak
+        if args.weak:  # every rank a whole H-row image stacked below the others
+            self.H, self.r0, self.r1 = H * world, rank * H, (rank + 1) * H
+        else:
+            self.H = H
+            self.r0, self.r1 = row_range(H, world, rank)
+        self.h = self.r1 - self.r0
+
+
+# ---- synthetic inputs -------------------------------------------------------------------------
 
 def synth_dirs(n, seed, radius=0.9):
     rng = np.random.default_rng(seed)
@@ -60,18 +114,24 @@ def synth_dirs(n, seed, radius=0.9):
     return (r * np.cos(th)).astype(np.float32), (r * np.sin(th)).astype(np.float32)
 
 
-def synth_stack(H, W, N, C, basis, lu, lv, seed, device):
-    """I[C, N, H*W] fp32 = clip(round(B·a + N(0,2)), 0, 255) with smooth coefficient fields a."""
+def synth_stack(H, W, N, C, basis, lu, lv, seed, device, rows=None):
+    """Rows [r0, r1) of I[C, N, H*W] fp32 = clip(round(B·a + N(0,2)), 0, 255) with smooth coefficient
+    fields a(y, x) of the whole H×W image (identical on every rank; the noise is per row block)."""
+    import torch
+
     import rti
 
+    r0, r1 = rows or (0, H)
+    h = r1 - r0
     g = torch.Generator(device=device).manual_seed(seed)
+    gn = torch.Generator(device=device).manual_seed(seed * 7919 + r0)
     k = rti.basis_terms(basis)
-    B = torch.as_tensor(rti.design_matrix(lu, lv, basis), device=device, dtype=torch.float32)  # [N, k]
-    yy = torch.linspace(0, 1, H, device=device)[:, None]
+    B = rti.design_matrix(lu, lv, basis)  # [N, k] host fp64
+    yy = torch.linspace(0, 1, H, device=device)[r0:r1, None]
     xx = torch.linspace(0, 1, W, device=device)[None, :]
-    out = torch.empty((C, N, H * W), device=device, dtype=torch.float32)
+    out = torch.empty((C, N, h * W), device=device, dtype=torch.float32)
     for c in range(C):
-        a = torch.empty((k, H * W), device=device)
+        a = torch.empty((k, h * W), device=device)
         for j in range(k):
             f1, f2, p1, p2 = (torch.rand(4, generator=g, device=device) * torch.tensor([2.5, 2.5, 6.28, 6.28],
                                                                                       device=device)).tolist()
@@ -80,24 +140,13 @@ def synth_stack(H, W, N, C, basis, lu, lv, seed, device):
             a[j] = base + amp * s
         # element-wise accumulation: torch's fp32 GEMM returns wrong values for
         # [n,6] @ [6, 8294400] on this ROCm stack (tools/probe_matmul.py), so no library GEMM here
-        Bh = B.cpu().numpy()
         for n in range(N):
-            row = torch.randn(H * W, generator=g, device=device) * 2.0
+            row = torch.randn(h * W, generator=gn, device=device) * 2.0
             for j in range(k):
-                row.add_(a[j], alpha=float(Bh[n, j]))
+                row.add_(a[j], alpha=float(B[n, j]))
             out[c, n] = row.round_().clamp_(0, 255)
         del a
     return out
-
-
-def load_traffic(workload_key):
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    try:
-        with open(path) as f:
-            entry = json.load(f).get(workload_key) or {}
-        return entry.get("traffic_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
 
 
 def synth_cams(n, seed, H, W):
@@ -110,49 +159,82 @@ def synth_cams(n, seed, H, W):
                      rad * np.cos(th)], -1)
 
 
-def cpu_sample_rate(fn, units, budget_s):
-    fn()  # warm-up
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        fn()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            return units * reps / el / 1e6, reps, el
-
-
-def cpu_info():
+def load_traffic(workload_key):
+    path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([t.get("num_threads", 1) for t in threadpool_info() if t.get("user_api") == "blas"] or [1])
-    except Exception:  # pragma: no cover
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    name = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                name = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return int(threads), name
+        with open(path) as f:
+            entry = json.load(f).get(workload_key) or {}
+        return entry.get("traffic_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
-class FitWorkload:
-    """One step = one rti_fit_shared launch over the rank's whole stack."""
+def oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rti_oracle
 
-    def __init__(self, args, cfg, rank, dev):
+    return rti_oracle
+
+
+def sample_idx(P, n, seed):
+    rng = np.random.default_rng(seed)
+    if P <= n:
+        return np.arange(P)
+    return np.sort(rng.choice(P, n, replace=False))
+
+
+def coef_parity(got, ref):
+    """max over pixels of max_k |c - c_ref| / max(max_k |c_ref|, 1e-30)."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    scale = np.maximum(np.abs(ref).max(-1, keepdims=True), 1e-30)
+    return float((np.abs(got - ref) / scale).max())
+
+
+def int_table_parity(got, ref_float):
+    """int32 outputs (C truncation): exact match except where the fp64 value sits within 1e-4 of an
+    integer (the truncation may then fall either way)."""
+    ref_i = np.trunc(ref_float).astype(np.int64)
+    diff = np.asarray(got, np.int64) != ref_i
+    near = np.abs(ref_float - np.round(ref_float)) < 1e-4
+    return {"checked": int(diff.size), "mismatch": int(diff.sum()), "mismatch_not_near_integer": int((diff & ~near).sum()),
+            "ok": bool(not (diff & ~near).any())}
+
+
+# ---- workloads --------------------------------------------------------------------------------
+
+class Workload:
+    """Subclasses set units (this rank's work per step), total_units, alg_bytes (per launch),
+    metric, unit, desc and implement step(i), config(), parity() and cpu_fn()."""
+
+    dtype = "f32"
+
+    def roofline(self, kernel_ms):
+        gbs = self.alg_bytes / (kernel_ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": self.traffic(), "kernel_ms": round(kernel_ms, 4),
+                "alg_bytes_per_launch": self.alg_bytes}
+
+    def traffic(self):
+        return None
+
+
+class FitWorkload(Workload):
+    """One step = one rti_fit_shared launch over this rank's row block of the stack."""
+
+    def __init__(self, args, cfg, ctx):
+        import torch
+
         import rti
 
-        self.rti = rti
+        self.rti, self.args, self.ctx = rti, args, ctx
         _, H, W, N, C, basis, desc = cfg
-        self.H, self.W, self.N, self.C, self.basis, self.desc = H, W, N, C, basis, desc
+        self.W, self.N, self.C, self.basis, self.desc = W, N, C, basis, desc
         self.k = k = rti.basis_terms(basis)
-        self.P = P = H * W
-        self.args = args
+        self.P = P = ctx.h * W
+        dev = ctx.dev
         self.lu, self.lv = synth_dirs(N, seed=2)
-        self.I = synth_stack(H, W, N, C, basis, self.lu, self.lv, seed=1000 + rank, device=dev)
+        self.I = synth_stack(ctx.H, W, N, C, basis, self.lu, self.lv, seed=1000, device=dev, rows=(ctx.r0, ctx.r1))
         self.in_bytes = 4
         if args.in_dtype != "f32":  # integer-valued 0..255 stacks, as the reference's V channel (analysis.py:219)
             self.I = self.I.to(torch.uint8 if args.in_dtype == "u8" else torch.int32)
@@ -161,154 +243,351 @@ class FitWorkload:
         self.pinv_dev = torch.as_tensor(self.pinv64.astype(np.float32), device=dev)
         self.coef = torch.empty((C, P, k) if args.layout == "pixel" else (C, k, P), dtype=torch.float32, device=dev)
         self.units = P * N * C
+        self.total_units = ctx.H * W * N * C
         self.alg_bytes = float(self.in_bytes) * P * N * C + 4.0 * P * k * C  # stack read once + fp32 coefs written
-        self.metric = "Mpix*lights/sec PTM fit (4K, 100 lights)" if args.config == "c3" else f"Mpix*lights/sec {desc}"
+        self.metric = ("Mpix*lights/sec PTM fit (4K, 100 lights)" if args.config == "c3"
+                       else f"Mpix*lights/sec {desc}")
         self.unit = "Mpix*lights/s"
+        self.dtype = "f32" if args.in_dtype == "f32" else f"{args.in_dtype} in / f32 compute"
+        L = rti._lib
+        kern = rti.api._KERNELS[args.kernel] | (L.RTI_KERNEL_NONTEMPORAL if args.nontemporal else 0)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        fn = L.lib().rti_fit_shared
+        cargs = (ctypes.c_void_p(self.pinv_dev.data_ptr()), k, N, ctypes.c_void_p(self.I.data_ptr()),
+                 rti.api._IN_DTYPES[self.I.dtype], P, C, P, N * P, ctypes.c_void_p(self.coef.data_ptr()),
+                 rti.api._layout_id(args.layout), P * k, kern, stream)
 
-    def step(self, i):
-        self.rti.fit_shared_into(self.pinv_dev, self.I, self.coef, k=self.k, layout=self.args.layout,
-                                 kernel=self.args.kernel, nontemporal=self.args.nontemporal)
+        def step(i):
+            st = fn(*cargs)
+            if st:
+                L.check(st, "rti_fit_shared")
+
+        self.step = step
+
+    def traffic(self):
+        if self.ctx.world != 1 or self.ctx.weak:
+            return None  # the PMC figures in profiles/traffic.json are for the whole image
+        a = self.args
+        key = f"{a.config}-{a.kernel}-{a.layout}" + ("" if a.in_dtype == "f32" else f"-{a.in_dtype}")
+        return load_traffic(key)
 
     def config(self):
         return {"lights": self.N, "channels": self.C, "basis": self.basis, "k": self.k,
                 "coef_layout": self.args.layout, "kernel": self.args.kernel, "intensity_dtype": self.args.in_dtype}
 
-    def cpu_baseline(self, budget_s):
-        """Oracle restatement: fp64 pinv + fp32 NumPy matmul on light-major rows."""
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import rti_oracle as o
+    def coef_pk(self, c):
+        cc = self.coef[c]
+        return cc if self.args.layout == "pixel" else cc.T
 
-        rows = max(1, self.H // 10)
+    def parity(self):
+        o = oracle()
+        idx = sample_idx(self.P, 4096, 11 + self.ctx.rank)
+        worst = 0.0
+        for c in sorted({0, self.C - 1}):
+            I = self.I[c][:, idx].float().cpu().numpy()
+            ref = o.fit_shared(I, self.pinv64)
+            got = self.coef_pk(c)[idx].cpu().numpy()
+            worst = max(worst, coef_parity(got, ref))
+        return {"max_rel": worst, "tol": 1e-4, "ok": bool(worst <= 1e-4), "checked_px": int(len(idx)),
+                "vs": "oracle fit_shared (fp64 pinv, fp64 contraction)"}
+
+    def cpu_fn(self):
+        o = oracle()
+        rows = max(1, min(self.ctx.h, 216))
         sample = self.I[0, :, : rows * self.W].float().cpu().numpy()
-        rate, reps, el = cpu_sample_rate(lambda: o.fit_shared_f32(sample, self.pinv64), self.N * rows * self.W,
-                                         budget_s)
-        threads, name = cpu_info()
-        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
-                "sample": f"oracle fit_shared_f32 (fp64 pinv + fp32 NumPy matmul, channel 0) on {rows}x{self.W} px "
-                          f"x {self.N} lights, {reps} reps in {el:.1f}s; {name}"}
+        return (lambda: o.fit_shared_f32(sample, self.pinv64), self.N * rows * self.W,
+                f"oracle fit_shared_f32 (fp64 pinv + fp32 NumPy matmul, channel 0) on {rows}x{self.W} px x {self.N} "
+                f"lights")
 
 
-class RelightWorkload:
-    """One step = one rti_relight launch evaluating ONE (lu, lv) over the 4K coefficient maps (interactive)."""
+class FitResidualWorkload(FitWorkload):
+    """One step = one rti_fit_shared_residual launch: coefficients + per-pixel RMS residuals + per-workgroup
+    residual energy in one pass over the stack (fp64 accumulation)."""
 
-    def __init__(self, args, cfg, rank, dev):
+    def __init__(self, args, cfg, ctx):
+        import torch
+
+        super().__init__(args, cfg, ctx)
+        rti, L = self.rti, self.rti._lib
+        k, N, C, P = self.k, self.N, self.C, self.P
+        dev = ctx.dev
+        self.ginv = rti.gram_inverse(self.lu, self.lv, self.basis)
+        self.A64 = rti.design_matrix(self.lu, self.lv, self.basis)
+        self.A_dev = torch.as_tensor(self.A64, device=dev).contiguous()
+        self.ginv_dev = torch.as_tensor(self.ginv, device=dev).contiguous()
+        self.res = torch.empty((C, P), dtype=torch.float32, device=dev)
+        nb = int(L.lib().rti_fit_shared_residual_blocks(P))
+        self.partial = torch.zeros((C, nb), dtype=torch.float64, device=dev)
+        self.alg_bytes += 4.0 * P * C  # + fp32 residual map
+        self.metric = f"Mpix*lights/sec {self.desc}"
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        fn = L.lib().rti_fit_shared_residual
+        cargs = (ctypes.c_void_p(self.A_dev.data_ptr()), ctypes.c_void_p(self.ginv_dev.data_ptr()), k, N,
+                 ctypes.c_void_p(self.I.data_ptr()), rti.api._IN_DTYPES[self.I.dtype], P, C, P, N * P,
+                 ctypes.c_void_p(self.coef.data_ptr()), rti.api._layout_id(args.layout), P * k,
+                 ctypes.c_void_p(self.res.data_ptr()), ctypes.c_void_p(self.partial.data_ptr()), 0, stream)
+
+        def step(i):
+            st = fn(*cargs)
+            if st:
+                L.check(st, "rti_fit_shared_residual")
+
+        self.step = step
+        self.dtype = "f32 in / f64 accumulate / f32 out"
+
+    def traffic(self):
+        return None
+
+    def parity(self):
+        o = oracle()
+        idx = sample_idx(self.P, 4096, 13 + self.ctx.rank)
+        worst = worst_r = 0.0
+        for c in sorted({0, self.C - 1}):
+            I = self.I[c][:, idx].float().cpu().numpy().astype(np.float64)
+            ref = o.fit_shared(I, self.pinv64)
+            got = self.coef_pk(c)[idx].cpu().numpy()
+            worst = max(worst, coef_parity(got, ref))
+            rref, _ = o.fit_residual(I, self.A64, ref)
+            rg = self.res[c][idx].cpu().numpy()
+            worst_r = max(worst_r, float((np.abs(rg - rref) / np.maximum(rref, 1.0)).max()))
+        return {"max_rel": worst, "residual_max_rel": worst_r, "tol": 1e-4,
+                "ok": bool(worst <= 1e-4 and worst_r <= 1e-4), "checked_px": int(len(idx)),
+                "vs": "oracle fit_shared + fit_residual (fp64)"}
+
+
+class RelightWorkload(Workload):
+    """One step = one rti_relight launch evaluating ONE (lu, lv) over this rank's 4K coefficient rows
+    (interactive).  Cold (default): launches rotate over `--map-sets` coefficient-map sets and outputs,
+    so the bytes touched between two uses of one map exceed the 256 MiB Infinity Cache and every launch
+    streams from HBM (MI355X_MICROARCH.md §Infinity Cache); --map-sets 1 measures the L3-resident case."""
+
+    def __init__(self, args, cfg, ctx):
+        import torch
+
         import rti
 
-        self.rti = rti
+        self.rti, self.args, self.ctx = rti, args, ctx
         _, H, W, E, C, basis, desc = cfg
-        self.H, self.W, self.E, self.desc, self.basis = H, W, E, desc, basis
+        self.W, self.E, self.desc, self.basis = W, E, desc, basis
         self.k = k = rti.basis_terms(basis)
-        self.P = P = H * W
-        g = torch.Generator(device=dev).manual_seed(1000 + rank)
-        self.coef = (torch.rand((P, k), generator=g, device=dev) * 100 - 50).contiguous()
-        self.coef[:, k - 1] += 130
+        self.P = P = ctx.h * W
+        dev = ctx.dev
+        self.sets = max(1, args.map_sets)
+        g = torch.Generator(device=dev).manual_seed(1000 + ctx.rank)
+        self.coefs = []
+        for _ in range(self.sets):
+            c = (torch.rand((P, k), generator=g, device=dev) * 100 - 50).contiguous()
+            c[:, k - 1] += 130
+            self.coefs.append(c)
         rng = np.random.default_rng(4)
         r = np.sqrt(rng.random(E))
         th = 2 * np.pi * rng.random(E)
-        self.luv = torch.as_tensor(np.stack([r * np.cos(th), r * np.sin(th)], -1), device=dev).contiguous()
-        self.out = torch.empty((P,), dtype=torch.float32, device=dev)
+        self.luv_host = np.stack([r * np.cos(th), r * np.sin(th)], -1)
+        self.luv = torch.as_tensor(self.luv_host, device=dev).contiguous()
+        self.outs = [torch.empty((P,), dtype=torch.float32, device=dev) for _ in range(self.sets)]
         self.units = P
+        self.total_units = ctx.H * W
         self.alg_bytes = 4.0 * P * k + 4.0 * P  # coefficients read + fp32 image written, per eval
         self.metric = f"Mpix*evals/sec {desc}"
         self.unit = "Mpix*evals/s"
-        import ctypes
-
-        self.ctypes = ctypes
-        self.lib = rti._lib.lib()
-        self.bid = rti.basis_id(basis)
+        L = rti._lib
+        self.L, self.lib, self.bid = L, L.lib(), rti.basis_id(basis)
+        self.stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
     def step(self, i):
-        c = self.ctypes
-        e = i % self.E
-        st = self.lib.rti_relight(c.c_void_p(self.coef.data_ptr()), self.rti._lib.RTI_F32, self.bid, self.P,
-                                  self.rti._lib.RTI_COEF_PIXEL_MAJOR, c.c_void_p(self.luv.data_ptr() + 16 * e), 1,
-                                  c.c_void_p(self.out.data_ptr()), self.rti._lib.RTI_F32,
-                                  self.rti._lib.RTI_OUT_EVAL_MAJOR,
-                                  c.c_void_p(torch.cuda.current_stream().cuda_stream))
-        self.rti._lib.check(st, "rti_relight")
+        L, s = self.L, i % self.sets
+        st = self.lib.rti_relight(ctypes.c_void_p(self.coefs[s].data_ptr()), L.RTI_F32, self.bid, self.P,
+                                  L.RTI_COEF_PIXEL_MAJOR, ctypes.c_void_p(self.luv.data_ptr() + 16 * (i % self.E)), 1,
+                                  ctypes.c_void_p(self.outs[s].data_ptr()), L.RTI_F32, L.RTI_OUT_EVAL_MAJOR,
+                                  self.stream)
+        if st:
+            L.check(st, "rti_relight")
 
     def config(self):
-        return {"evals": self.E, "basis": self.basis, "k": self.k, "coef_layout": "pixel", "out": "f32"}
+        return {"evals": self.E, "basis": self.basis, "k": self.k, "coef_layout": "pixel", "out": "f32",
+                "map_sets": self.sets, "cache": "cold (working set between reuses > 256 MiB L3)" if self.cold()
+                else "L3-resident (one map set re-read every launch)"}
 
-    def cpu_baseline(self, budget_s):
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import rti_oracle as o
+    def cold(self):
+        return self.sets * (self.alg_bytes) > 300 * 2 ** 20
 
-        rows = max(1, self.H // 10)
-        c = self.coef[: rows * self.W].cpu().numpy()
-        lu, lv = self.luv[0].cpu().numpy()
-        rate, reps, el = cpu_sample_rate(lambda: o.relight(c, self.basis, lu, lv), rows * self.W, budget_s)
-        threads, name = cpu_info()
-        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
-                "sample": f"oracle relight (fp64 NumPy) on {rows}x{self.W} px x 1 eval, {reps} reps in {el:.1f}s; "
-                          f"{name}"}
+    def roofline(self, kernel_ms):
+        r = super().roofline(kernel_ms)
+        if not self.cold():
+            r["bound"] = "l3"  # the maps stay in the 256 MiB Infinity Cache between launches
+        return r
+
+    def parity(self):
+        import torch
+
+        o = oracle()
+        self.step(7)
+        torch.cuda.synchronize(self.ctx.dev)
+        s = 7 % self.sets
+        idx = sample_idx(self.P, 65536, 5)
+        lu, lv = self.luv_host[7 % self.E]
+        ref = o.relight(self.coefs[s][idx].cpu().numpy(), self.basis, lu, lv)[0]
+        got = self.outs[s][idx].cpu().numpy()
+        err = float((np.abs(got - ref) / np.maximum(np.abs(ref), 255)).max())
+        return {"max_rel": err, "tol": 1e-4, "ok": bool(err <= 1e-4), "checked_px": int(len(idx)),
+                "vs": "oracle relight (fp64)"}
+
+    def cpu_fn(self):
+        o = oracle()
+        rows = max(1, min(self.ctx.h, 216))
+        c = self.coefs[0][: rows * self.W].cpu().numpy()
+        lu, lv = self.luv_host[0]
+        return (lambda: o.relight(c, self.basis, lu, lv), rows * self.W,
+                f"oracle relight (fp64 NumPy) on {rows}x{self.W} px x 1 eval")
 
 
-class PerPixelWorkload:
+class FrameWorkload(RelightWorkload):
+    """One step = one rti_relight_frame launch: the image relighting_event shows for one cursor position
+    (interactive_relighting.py:31-38), from device-resident coefficient maps and HSV ROI."""
+
+    def __init__(self, args, cfg, ctx):
+        import torch
+
+        super().__init__(args, cfg, ctx)
+        dev = ctx.dev
+        g = torch.Generator(device=dev).manual_seed(2000 + ctx.rank)
+        self.hsv = torch.randint(0, 256, (self.P, 3), generator=g, device=dev, dtype=torch.uint8)
+        self.bgrs = [torch.empty((self.P, 3), dtype=torch.uint8, device=dev) for _ in range(self.sets)]
+        self.alg_bytes = 4.0 * self.P * self.k + 3.0 * self.P + 3.0 * self.P  # coefficients + HSV in, BGR out
+        self.dtype = "f32 eval -> u8 BGR"
+
+    def step(self, i):
+        L, s = self.L, i % self.sets
+        lu, lv = self.luv_host[i % self.E]
+        st = self.lib.rti_relight_frame(ctypes.c_void_p(self.coefs[s].data_ptr()), L.RTI_F32, self.bid,
+                                        L.RTI_COEF_PIXEL_MAJOR, self.P, float(lu), float(lv),
+                                        ctypes.c_void_p(self.hsv.data_ptr()), ctypes.c_void_p(self.bgrs[s].data_ptr()),
+                                        self.stream)
+        if st:
+            L.check(st, "rti_relight_frame")
+
+    def config(self):
+        c = super().config()
+        c.update({"events": self.E, "out": "uint8 BGR [P][3]"})
+        c.pop("evals", None)
+        return c
+
+    def parity(self):
+        import torch
+
+        o = oracle()
+        self.step(7)
+        torch.cuda.synchronize(self.ctx.dev)
+        s = 7 % self.sets
+        rows = min(self.ctx.h, 32)
+        n = rows * self.W
+        lu, lv = self.luv_host[7 % self.E]
+        v = o.relight(self.coefs[s][:n].cpu().numpy(), self.basis, lu, lv).reshape(rows, self.W)
+        ref = o.relighting_event_image(np.trunc(v).astype(np.int32), self.hsv[:n].cpu().numpy().reshape(rows, self.W, 3))
+        got = self.bgrs[s][:n].cpu().numpy().reshape(rows, self.W, 3)
+        near = np.abs(v - np.round(v)) < 1e-4  # fp32 evaluation vs fp64 truncation
+        bad = (got != ref).any(-1) & ~near
+        return {"mismatch_not_near_integer": int(bad.sum()), "checked_px": int(n), "ok": bool(not bad.any()),
+                "vs": "oracle relight + clip + HSV2BGR restatement"}
+
+    def cpu_fn(self):
+        o = oracle()
+        rows = max(1, min(self.ctx.h, 216))
+        c = self.coefs[0][: rows * self.W].cpu().numpy()
+        hsv = self.hsv[: rows * self.W].cpu().numpy().reshape(rows, self.W, 3)
+        lu, lv = self.luv_host[0]
+
+        def one():
+            v = o.relight(c, self.basis, lu, lv).reshape(rows, self.W)
+            return o.relighting_event_image(np.trunc(v).astype(np.int32), hsv)
+
+        return one, rows * self.W, f"oracle relight + clip + HSV2BGR (NumPy) on {rows}x{self.W} px x 1 event"
+
+
+class PerPixelWorkload(Workload):
     """One step = one rti_fit_perpixel_cam launch (directions from cameras, fp64 normal equations)."""
 
-    def __init__(self, args, cfg, rank, dev):
+    dtype = "f32 in / f64 solve"
+
+    def __init__(self, args, cfg, ctx):
+        import torch
+
         import rti
 
-        self.rti = rti
+        self.rti, self.args, self.ctx = rti, args, ctx
         _, H, W, N, C, basis, desc = cfg
-        self.H, self.W, self.N, self.desc = H, W, N, desc
-        self.P = P = H * W
-        self.cams = synth_cams(N, 6, H, W)
+        self.W, self.N, self.desc = W, N, desc
+        self.P = P = ctx.h * W
+        dev = ctx.dev
+        self.cams = synth_cams(N, 6, ctx.H, W)
         lu, lv = synth_dirs(N, seed=2)
-        self.I = synth_stack(H, W, N, 1, "ptm", lu, lv, seed=1000 + rank, device=dev)[0]  # [N, P]
+        self.I = synth_stack(ctx.H, W, N, 1, "ptm", lu, lv, seed=1000, device=dev, rows=(ctx.r0, ctx.r1))[0]
         self.cams_d = torch.as_tensor(self.cams, device=dev).contiguous()
         self.coef = torch.empty((P, 6), dtype=torch.float32, device=dev)
         self.units = P * N
+        self.total_units = ctx.H * W * N
         self.alg_bytes = 4.0 * P * N + 4.0 * P * 6
         self.metric = f"Mpix*lights/sec {desc}"
         self.unit = "Mpix*lights/s"
-        import ctypes
+        L = rti._lib
+        fn = L.lib().rti_fit_perpixel_cam
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        cargs = (ctypes.c_void_p(self.cams_d.data_ptr()), N, ctypes.c_void_p(self.I.data_ptr()), L.RTI_F32, ctx.h, W,
+                 P, 0.0, float(ctx.r0), -1.0, ctypes.c_void_p(self.coef.data_ptr()), L.RTI_F32,
+                 L.RTI_COEF_PIXEL_MAJOR, stream)
 
-        self.ctypes = ctypes
-        self.lib = rti._lib.lib()
+        def step(i):
+            st = fn(*cargs)
+            if st:
+                L.check(st, "rti_fit_perpixel_cam")
 
-    def step(self, i):
-        c = self.ctypes
-        L = self.rti._lib
-        st = self.lib.rti_fit_perpixel_cam(c.c_void_p(self.cams_d.data_ptr()), self.N, c.c_void_p(self.I.data_ptr()),
-                                           L.RTI_F32, self.H, self.W, self.P, 0.0, 0.0, -1.0,
-                                           c.c_void_p(self.coef.data_ptr()), L.RTI_F32, L.RTI_COEF_PIXEL_MAJOR,
-                                           c.c_void_p(torch.cuda.current_stream().cuda_stream))
-        L.check(st, "rti_fit_perpixel_cam")
+        self.step = step
 
     def config(self):
         return {"lights": self.N, "basis": "ptm", "k": 6, "coef_layout": "pixel", "geometry": "per-pixel cameras"}
 
-    def cpu_baseline(self, budget_s):
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import rti_oracle as o
+    def parity(self):
+        o = oracle()
+        idx = sample_idx(self.P, 2048, 17)
+        ys, xs = np.divmod(idx, self.W)
+        lu, lv = o.light_dirs_for_pixels(self.cams, xs, ys + self.ctx.r0)
+        ref = o.fit_perpixel(lu, lv, self.I[:, idx].cpu().numpy().T)
+        err = coef_parity(self.coef[idx].cpu().numpy(), ref)
+        return {"max_rel": err, "tol": 1e-4, "ok": bool(err <= 1e-4), "checked_px": int(len(idx)),
+                "vs": "oracle fit_perpixel (batched fp64 SVD, reference semantics)"}
 
-        npx = 4096
+    def cpu_fn(self):
+        o = oracle()
+        npx = min(4096, self.P)
         ys, xs = np.divmod(np.arange(npx), self.W)
-        lu, lv = o.light_dirs_for_pixels(self.cams, xs, ys)
+        lu, lv = o.light_dirs_for_pixels(self.cams, xs, ys + self.ctx.r0)
         I = self.I[:, :npx].cpu().numpy().T
-        rate, reps, el = cpu_sample_rate(lambda: o.fit_perpixel(lu, lv, I), npx * self.N, budget_s)
-        threads, name = cpu_info()
-        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
-                "sample": f"oracle fit_perpixel (batched fp64 NumPy SVD, reference semantics) on {npx} px x "
-                          f"{self.N} lights, {reps} reps in {el:.1f}s; {name}"}
+        return (lambda: o.fit_perpixel(lu, lv, I), npx * self.N,
+                f"oracle fit_perpixel (batched fp64 NumPy SVD, reference semantics) on {npx} px x {self.N} lights")
 
 
-class OperatorWorkload:
-    """One step = one rti_apply_operator launch: RBF operator (E = 100x100 grid) over the ROI stack -> int32."""
+def grid_queries():
+    xf = np.around(np.mgrid[-1:1:0.02, -1:1:0.02][1], 2)[0]
+    return np.tile(xf, xf.size), np.repeat(xf, xf.size)
 
-    def __init__(self, args, cfg, rank, dev):
+
+class OperatorWorkload(Workload):
+    """One step = one rti_apply_operator launch: RBF operator (E = 100x100 grid) over this rank's ROI rows -> int32."""
+
+    def __init__(self, args, cfg, ctx):
+        import torch
+
         import rti
 
-        self.rti = rti
+        self.rti, self.args, self.ctx = rti, args, ctx
         _, H, W, N, C, basis, desc = cfg
-        self.H, self.W, self.N, self.desc = H, W, N, desc
-        self.P = P = H * W
+        self.W, self.N, self.desc = W, N, desc
+        self.P = P = ctx.h * W
+        dev = ctx.dev
         self.lu, self.lv = synth_dirs(N, seed=2)
-        self.I = synth_stack(H, W, N, 1, "ptm", self.lu, self.lv, seed=1000 + rank, device=dev)[0]  # [N, P]
-        xf = np.around(np.mgrid[-1:1:0.02, -1:1:0.02][1], 2)[0]
-        self.qu, self.qv = np.tile(xf, xf.size), np.repeat(xf, xf.size)
+        self.I = synth_stack(ctx.H, W, N, 1, "ptm", self.lu, self.lv, seed=1000, device=dev,
+                             rows=(ctx.r0, ctx.r1))[0]  # [N, P]
+        self.qu, self.qv = grid_queries()
         self.E = E = self.qu.size
         self.op64 = rti.rbf_operator(self.lu, self.lv, self.qu, self.qv)  # [N, E] fp64 (host, one-time)
         self.precision = args.op_precision
@@ -317,76 +596,92 @@ class OperatorWorkload:
             self.hi, self.lo, self.Kp, self.inv = rti.api.split_operator_f16(self.op64, dev)
         self.out = torch.empty((E, P), dtype=torch.int32, device=dev)
         self.units = P * E
+        self.total_units = ctx.H * W * E
         self.alg_bytes = 4.0 * P * N + 4.0 * P * E  # stack read once + int32 tables written
         self.flops = 2.0 * E * N * P
         self.metric = f"Mpix*evals/sec {desc}"
         self.unit = "Mpix*evals/s"
-        import ctypes
-
-        self.ctypes = ctypes
-        self.lib = rti._lib.lib()
+        self.dtype = ("f32 operator as 2 x f16 (f16 MFMA, f32 accumulate) -> int32" if self.precision == "split16"
+                      else "f32 (MFMA) -> int32")
+        L = rti._lib
+        self.L, self.lib = L, L.lib()
+        self.stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
     def step(self, i):
-        c = self.ctypes
-        L = self.rti._lib
-        stream = c.c_void_p(torch.cuda.current_stream().cuda_stream)
+        c, L = ctypes, self.L
         if self.precision == "split16":
             st = self.lib.rti_apply_operator_f16(c.c_void_p(self.hi.data_ptr()), c.c_void_p(self.lo.data_ptr()),
                                                  self.Kp, self.inv, self.E, self.N, c.c_void_p(self.I.data_ptr()),
                                                  L.RTI_F32, self.P, 1, self.P, self.N * self.P,
                                                  c.c_void_p(self.out.data_ptr()), L.RTI_I32, self.P, self.E * self.P,
-                                                 stream)
-            L.check(st, "rti_apply_operator_f16")
+                                                 self.stream)
+            if st:
+                L.check(st, "rti_apply_operator_f16")
             return
         st = self.lib.rti_apply_operator(c.c_void_p(self.op.data_ptr()), self.E, self.N, self.E,
                                          c.c_void_p(self.I.data_ptr()), L.RTI_F32, self.P, 1, self.P, self.N * self.P,
-                                         c.c_void_p(self.out.data_ptr()), L.RTI_I32, self.P, self.E * self.P, stream)
-        L.check(st, "rti_apply_operator")
+                                         c.c_void_p(self.out.data_ptr()), L.RTI_I32, self.P, self.E * self.P, self.stream)
+        if st:
+            L.check(st, "rti_apply_operator")
 
     def config(self):
         return {"lights": self.N, "evals": self.E, "basis": "rbf-linear", "out": "int32 tables [E][P]",
                 "operator_precision": self.precision}
+
+    def traffic(self):
+        if self.ctx.world != 1 or self.ctx.weak:
+            return None
+        return load_traffic(f"{self.args.config}-{self.precision}")
 
     def roofline(self, kernel_ms):
         ach = self.flops / (kernel_ms * 1e-3) / 1e12
         if self.precision == "split16":
             # two f16 MFMA products per multiply-add put the compute at 2 x 3.2e11 x 1.12 flop per launch
             # (~0.3 ms at the dense f16 peak), so the E x P int32 table writes (6.4 GB) bound it: HBM roofline
-            gbs = self.alg_bytes / (kernel_ms * 1e-3) / 1e9
-            return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(kernel_ms, 4),
-                    "alg_bytes_per_launch": self.alg_bytes, "alg_flops_per_launch": self.flops,
-                    "mfma_f16_TFLOPs_issued": round(2 * self.flops * (self.Kp / self.N) / (kernel_ms * 1e-3) / 1e12, 1),
-                    "mfma_f16_peak": 2516.6}
+            r = super().roofline(kernel_ms)
+            r.update({"alg_flops_per_launch": self.flops,
+                      "mfma_f16_TFLOPs_issued": round(2 * self.flops * (self.Kp / self.N) / (kernel_ms * 1e-3) / 1e12, 1),
+                      "mfma_f16_peak": 2516.6})
+            return r
         return {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None, "kernel_ms": round(kernel_ms, 4),
                 "alg_flops_per_launch": self.flops, "alg_bytes_per_launch": self.alg_bytes,
                 "hbm_GBps": round(self.alg_bytes / (kernel_ms * 1e-3) / 1e9, 1)}
 
-    def cpu_baseline(self, budget_s):
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        npx = 256
+    def parity(self):
+        idx = sample_idx(self.P, 512, 19)
+        ref = self.op64.T @ self.I[:, idx].cpu().numpy().astype(np.float64)  # [E, n]
+        got = self.out[:, idx].cpu().numpy()
+        r = int_table_parity(got, ref)
+        r["vs"] = "fp64 operator product (oracle rbf_operator-equivalent) truncated to int32"
+        return r
+
+    def cpu_fn(self):
+        npx = min(256, self.P)
         I = self.I[:, :npx].cpu().numpy().astype(np.float64)
         op = self.op64
-        rate, reps, el = cpu_sample_rate(lambda: (op.T @ I).astype(np.int32), npx * self.E, budget_s)
-        threads, name = cpu_info()
-        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
-                "sample": f"NumPy fp64 operator product (the SciPy-Rbf-equivalent grid) on {npx} px x {self.E} "
-                          f"evals, {reps} reps in {el:.1f}s; {name}"}
+        return (lambda: (op.T @ I).astype(np.int32), npx * self.E,
+                f"NumPy fp64 operator product (the SciPy-Rbf-equivalent grid) on {npx} px x {self.E} evals")
 
 
-class RbfPerPixelWorkload:
-    """One step = one rti_rbf_perpixel launch over the ROI: per-pixel fp64 solve + 10^4 evaluations."""
+class RbfPerPixelWorkload(Workload):
+    """One step = one rti_rbf_perpixel launch over this rank's ROI rows: per-pixel fp64 solve + 10^4 evaluations."""
 
-    def __init__(self, args, cfg, rank, dev):
+    dtype = "f64 -> int32"
+
+    def __init__(self, args, cfg, ctx):
+        import torch
+
         import rti
 
-        self.rti = rti
+        self.rti, self.args, self.ctx = rti, args, ctx
         _, H, W, N, C, basis, desc = cfg
-        self.H, self.W, self.N, self.desc = H, W, N, desc
-        self.P = P = H * W
-        cams = synth_cams(N, 6, H, W)
+        self.W, self.N, self.desc = W, N, desc
+        self.P = P = ctx.h * W
+        dev = ctx.dev
+        cams = synth_cams(N, 6, ctx.H, W)
         ys, xs = np.divmod(np.arange(P), W)
+        ys = ys + ctx.r0
         dx = cams[None, :, 0] - xs[:, None]
         dy = cams[None, :, 1] - ys[:, None]
         nrm = np.sqrt(dx * dx + dy * dy + cams[None, :, 2] ** 2)
@@ -394,147 +689,248 @@ class RbfPerPixelWorkload:
         self.lv_h = (dy / nrm).astype(np.float32)
         self.lu = torch.as_tensor(self.lu_h, device=dev)
         self.lv = torch.as_tensor(self.lv_h, device=dev)
-        rng = np.random.default_rng(7 + rank)
+        rng = np.random.default_rng(7 + ctx.rank)
         self.I_h = rng.integers(0, 256, (P, N)).astype(np.int32)
         self.I = torch.as_tensor(self.I_h, device=dev)
-        xf = np.around(np.mgrid[-1:1:0.02, -1:1:0.02][1], 2)[0]
-        self.qu, self.qv = np.tile(xf, xf.size), np.repeat(xf, xf.size)
+        self.qu, self.qv = grid_queries()
         self.E = E = self.qu.size
         self.luv = torch.as_tensor(np.stack([self.qu, self.qv], -1), device=dev).contiguous()
         self.out = torch.empty((E, P), dtype=torch.int32, device=dev)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.units = P * E
+        self.total_units = ctx.H * W * E
         self.alg_bytes = 12.0 * P * N + 4.0 * P * E
         self.flops = P * (2.0 / 3.0 * N ** 3 + 5.0 * N * N + 8.0 * N * E)  # LU + A build + evaluation (fp64)
         self.metric = f"Mpix*evals/sec {desc}"
         self.unit = "Mpix*evals/s"
-        import ctypes
-
-        self.ctypes = ctypes
-        self.lib = rti._lib.lib()
+        L = rti._lib
+        self.L, self.lib = L, L.lib()
+        self.stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
     def step(self, i):
-        c = self.ctypes
-        L = self.rti._lib
+        c, L = ctypes, self.L
         st = self.lib.rti_rbf_perpixel(c.c_void_p(self.lu.data_ptr()), c.c_void_p(self.lv.data_ptr()),
                                        c.c_void_p(self.I.data_ptr()), L.RTI_I32, self.N, self.P,
                                        c.c_void_p(self.luv.data_ptr()), self.E, c.c_void_p(self.out.data_ptr()),
                                        L.RTI_I32, L.RTI_OUT_EVAL_MAJOR, c.c_void_p(self.status.data_ptr()),
-                                       c.c_void_p(torch.cuda.current_stream().cuda_stream))
-        L.check(st, "rti_rbf_perpixel")
+                                       self.stream)
+        if st:
+            L.check(st, "rti_rbf_perpixel")
 
     def config(self):
         return {"lights": self.N, "evals": self.E, "basis": "rbf-linear per-pixel", "out": "int32 tables [E][P]"}
 
     def roofline(self, kernel_ms):
         ach = self.flops / (kernel_ms * 1e-3) / 1e12
-        return {"bound": "fp64-valu", "achieved": round(ach, 2), "peak": 78.6, "unit": "TFLOP/s",
-                "frac": round(ach / 78.6, 4), "traffic": None, "kernel_ms": round(kernel_ms, 4),
+        return {"bound": "fp64-valu", "achieved": round(ach, 2), "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP64_VALU_PEAK_TFLOPS, 4), "traffic": None, "kernel_ms": round(kernel_ms, 4),
                 "alg_flops_per_launch": self.flops, "alg_bytes_per_launch": self.alg_bytes}
 
-    def cpu_baseline(self, budget_s):
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import rti_oracle as o
+    def parity(self):
+        o = oracle()
+        idx = sample_idx(self.P, 8, 23)
+        ref = np.stack([o.rbf_linear(self.lu_h[p], self.lv_h[p], self.I_h[p], self.qu, self.qv) for p in idx], -1)
+        got = self.out[:, idx].cpu().numpy()
+        r = int_table_parity(got, ref)
+        r["vs"] = "oracle rbf_linear (SciPy-equivalent fp64 solve + cdist eval)"
+        return r
 
+    def cpu_fn(self):
+        o = oracle()
         npx = 16
+
         def run():
             for p in range(npx):
                 o.rbf_linear(self.lu_h[p], self.lv_h[p], self.I_h[p], self.qu, self.qv)
-        rate, reps, el = cpu_sample_rate(run, npx * self.E, budget_s)
-        threads, name = cpu_info()
-        return {"value": round(rate, 3), "unit": self.unit, "cores": threads, "kind": "port",
-                "sample": f"oracle rbf_linear (SciPy-equivalent fp64 solve + cdist eval) on {npx} px x {self.E} "
-                          f"evals, {reps} reps in {el:.1f}s; {name}"}
+
+        return run, npx * self.E, f"oracle rbf_linear (SciPy-equivalent fp64 solve + cdist eval) on {npx} px x {self.E} evals"
 
 
-class FrameWorkload(RelightWorkload):
-    """One step = one rti_relight_frame launch: the image relighting_event shows for one cursor position
-    (interactive_relighting.py:31-38), from device-resident coefficient maps and HSV ROI."""
-
-    def __init__(self, args, cfg, rank, dev):
-        super().__init__(args, cfg, rank, dev)
-        g = torch.Generator(device=dev).manual_seed(2000 + rank)
-        self.hsv = torch.randint(0, 256, (self.P, 3), generator=g, device=dev, dtype=torch.uint8)
-        self.bgr = torch.empty((self.P, 3), dtype=torch.uint8, device=dev)
-        self.luv_host = self.luv.cpu().numpy()
-        self.alg_bytes = 4.0 * self.P * self.k + 3.0 * self.P + 3.0 * self.P  # coefficients + HSV in, BGR out
-
-    def step(self, i):
-        c = self.ctypes
-        lu, lv = self.luv_host[i % self.E]
-        st = self.lib.rti_relight_frame(c.c_void_p(self.coef.data_ptr()), self.rti._lib.RTI_F32, self.bid,
-                                        self.rti._lib.RTI_COEF_PIXEL_MAJOR, self.P, float(lu), float(lv),
-                                        c.c_void_p(self.hsv.data_ptr()), c.c_void_p(self.bgr.data_ptr()),
-                                        c.c_void_p(torch.cuda.current_stream().cuda_stream))
-        self.rti._lib.check(st, "rti_relight_frame")
-
-    def config(self):
-        return {"events": self.E, "basis": self.basis, "k": self.k, "coef_layout": "pixel",
-                "out": "uint8 BGR [P][3]"}
-
-    def cpu_baseline(self, budget_s):
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import rti_oracle as o
-
-        rows = max(1, self.H // 10)
-        c = self.coef[: rows * self.W].cpu().numpy()
-        hsv = self.hsv[: rows * self.W].cpu().numpy().reshape(rows, self.W, 3)
-        lu, lv = self.luv_host[0]
-
-        def one():
-            v = o.relight(c, self.basis, lu, lv).reshape(rows, self.W)
-            return o.relighting_event_image(np.trunc(v).astype(np.int32), hsv)
-
-        rate, reps, el = cpu_sample_rate(one, rows * self.W, budget_s)
-        threads, name = cpu_info()
-        return {"value": round(rate, 1), "unit": self.unit, "cores": threads, "kind": "port",
-                "sample": f"oracle relight + clip + HSV2BGR (NumPy) on {rows}x{self.W} px x 1 event, {reps} reps in "
-                          f"{el:.1f}s; {name}"}
+WORKLOADS = {"fit": FitWorkload, "fit_residual": FitResidualWorkload, "relight": RelightWorkload,
+             "perpixel": PerPixelWorkload, "frame": FrameWorkload, "operator": OperatorWorkload,
+             "rbf_perpixel": RbfPerPixelWorkload}
 
 
-WORKLOADS = {"fit": FitWorkload, "relight": RelightWorkload, "perpixel": PerPixelWorkload, "frame": FrameWorkload,
-             "operator": OperatorWorkload, "rbf_perpixel": RbfPerPixelWorkload}
+# ---- CPU baseline -----------------------------------------------------------------------------
+
+def cgroup_cpus():
+    """CPUs granted by the cgroup quota (cpu.max), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        return None
 
 
-def main():
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def time_cpu(fn, units, budget_s):
+    """1 warm-up, then repeats until >= 5 runs and >= budget_s; rate from the median run."""
+    fn()
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < 5 or time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    return units / float(np.median(times)) / 1e6, len(times)
+
+
+def cpu_baseline(wl, budget_s):
+    from threadpoolctl import threadpool_limits
+
+    fn, units, desc = wl.cpu_fn()
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    threads = min(aff, quota) if quota else aff
+    with threadpool_limits(threads):
+        rate_n, reps_n = time_cpu(fn, units, budget_s / 2)
+    with threadpool_limits(1):
+        rate_1, reps_1 = time_cpu(fn, units, budget_s / 2)
+    return {"value": round(rate_n, 3), "unit": wl.unit, "cores": threads, "kind": "port",
+            "value_1thread": round(rate_1, 3),
+            "sample": f"{desc}; median of {reps_n} runs at {threads} BLAS threads (sched_getaffinity {aff}"
+                      f"{f', cgroup quota {quota}' if quota else ''}) and of {reps_1} runs at 1 thread, after 1 "
+                      f"warm-up each; {cpu_model()}"}
+
+
+# ---- multi-GPU legs ---------------------------------------------------------------------------
+
+def allgather_legs(wl, ctx, reps=5):
+    """RCCL all-gather of this rank's coefficient rows into the whole [H, W, k] map, and the row-chunked
+    fit with each chunk's all-gather overlapped with the next chunk's fit (block-cyclic rows, so every
+    chunk lands in place).  Returns (allgather_ms, overlapped_ms) maxed over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from rti.parallel import RowTiledFitter, gather_rows
+
+    dev = ctx.dev
+    local = wl.coef[0].reshape(ctx.h, wl.W, wl.k) if wl.args.layout == "pixel" else \
+        wl.coef[0].T.reshape(ctx.h, wl.W, wl.k).contiguous()
+    for _ in range(2):
+        gather_rows(local, ctx.H)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        gather_rows(local, ctx.H)
+    torch.cuda.synchronize(dev)
+    gather_ms = (time.perf_counter() - t0) / reps * 1e3
+    chunks = next(c for c in (4, 3, 2, 1) if ctx.h % c == 0)  # cyclic blocks of h/chunks rows (2160/8 = 270: 3)
+    fitter = RowTiledFitter(wl.I[0].reshape(wl.N, ctx.h, wl.W), wl.lu, wl.lv, ctx.H, basis=wl.basis, chunks=chunks,
+                            partition="cyclic")
+    for _ in range(2):
+        fitter()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fitter()
+    torch.cuda.synchronize(dev)
+    e2e_ms = (time.perf_counter() - t0) / reps * 1e3
+    return gather_ms, e2e_ms, chunks
+
+
+def reduce_max(vals, ctx, backend):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(vals, dtype=torch.float64, device=ctx.dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t]
+
+
+def gather_vals(v, ctx, backend):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([v], dtype=torch.float64, device=ctx.dev if backend == "nccl" else "cpu")
+    out = [torch.empty_like(t) for _ in range(ctx.world)]
+    dist.all_gather(out, t)
+    return [float(x[0]) for x in out]
+
+
+# ---- main -------------------------------------------------------------------------------------
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default 20 (fit) / 1000 (relight) / 10 (per-pixel)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma"])
+    ap.add_argument("--weak", action="store_true", help="every rank fits a whole H-row image (weak scaling)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma", "tile"])
     ap.add_argument("--layout", default="pixel", choices=["pixel", "planar"])
     ap.add_argument("--nontemporal", action="store_true")
     ap.add_argument("--in-dtype", default="f32", choices=["f32", "u8", "i32"],
                     help="intensity stack type for fit configs (BASELINE's metric is fp32)")
     ap.add_argument("--op-precision", default="split16", choices=["split16", "fp32"],
                     help="c7: operator as two fp16 halves on f16 MFMA (default) or fp32 on f32 MFMA")
-    ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of the maps")
+    ap.add_argument("--map-sets", type=int, default=3,
+                    help="c5/c9: coefficient-map sets rotated over launches (3 = HBM-cold, 1 = L3-resident)")
+    ap.add_argument("--no-allgather", action="store_true", help="N>1: skip the RCCL all-gather legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-parity", action="store_true", help="skip the in-run parity check")
+    ap.add_argument("--cpu-budget", type=float, default=16.0, help="seconds of CPU baseline (half per thread count)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo lets ranks share one GPU in rehearsals")
-    args = ap.parse_args()
+    ap.add_argument("--plan", action="store_true",
+                    help="print the rank/row plan only (no device work; CPU tests of the launcher)")
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    maybe_spawn(args)
     cfg = CONFIGS[args.config]
     kind = cfg[0]
     if args.steps is None:
-        args.steps = {"fit": 20, "relight": 1000, "frame": 1000, "perpixel": 10, "operator": 10, "rbf_perpixel": 3}[kind]
+        args.steps = DEFAULT_STEPS[kind]
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = max(1, torch.cuda.device_count())
-    dev = torch.device("cuda", local % ndev)
-    torch.cuda.set_device(dev)
+    backend = "gloo" if args.plan else args.dist_backend
+    if args.plan:
+        dev = torch.device("cpu")
+    else:
+        ndev = max(1, torch.cuda.device_count())
+        dev = torch.device("cuda", local % ndev)
+        torch.cuda.set_device(dev)
     if world > 1:
-        if args.dist_backend == "nccl":
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    ctx = Ctx(args, cfg[1], rank, world, dev)
+    if args.plan:
+        rows = [[int(a), int(b)] for a, b in zip(gather_vals(ctx.r0, ctx, "gloo"), gather_vals(ctx.r1, ctx, "gloo"))] \
+            if world > 1 else [[ctx.r0, ctx.r1]]
+        if rank == 0:
+            print(json.dumps({"metric": None, "value": None, "n_gpus": world, "plan_only": True,
+                              "scaling": "weak" if args.weak else "strong",
+                              "config": {"workload": cfg[6], "H": ctx.H, "W": cfg[2], "H_per_rank": ctx.h,
+                                         "rows_per_rank": rows}}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     import rti
 
     rti.load()
-    wl = WORKLOADS[kind](args, cfg, rank, dev)
+    wl = WORKLOADS[kind](args, cfg, ctx)
     torch.cuda.synchronize(dev)
 
     for i in range(args.warmup):
@@ -552,62 +948,48 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    # kernel duration for the roofline: HIP events around each launch, on the launch stream,
-    # in a separate pass so the events do not add gaps to the timed region
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for i in range(args.steps):
-        ev[i][0].record(stream)
+    elapsed = time.perf_counter() - t0
+
+    # kernel duration for the roofline: HIP events around each launch on the launch
+    # stream, 10 warm-ups then the median of 50, in a separate pass so the events add no gaps above
+    for i in range(10):
         wl.step(i)
-        ev[i][1].record(stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
+    for i, (a, b) in enumerate(ev):
+        a.record(stream)
+        wl.step(i)
+        b.record(stream)
     torch.cuda.synchronize(dev)
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kms = np.array([a.elapsed_time(b) for a, b in ev])
+    kernel_ms = float(np.median(kms))
+    kernel_ms_rank = [kernel_ms]
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+        kernel_ms_rank = gather_vals(kernel_ms, ctx, backend)
+        elapsed, kernel_ms = reduce_max([elapsed, kernel_ms], ctx, backend)
+
+    parity = None
+    if not args.no_parity:
+        parity = wl.parity()
+        if world > 1:  # every rank checked its own rows; report the worst
+            worst = reduce_max([parity.get("max_rel", 0.0), 0.0 if parity["ok"] else 1.0], ctx, backend)
+            if "max_rel" in parity:
+                parity["max_rel"] = worst[0]
+            parity["ok"] = worst[1] == 0.0
+            parity["ranks"] = world
 
     gather_ms = e2e_ms = None
-    if args.allgather and world > 1 and kind == "fit":
-        from rti.parallel import gather_rows
+    if world > 1 and kind == "fit" and not args.no_allgather:
+        gather_ms, e2e_ms, n_chunks = reduce_max(list(allgather_legs(wl, ctx)), ctx, backend)
 
-        H, W, k = wl.H, wl.W, wl.k
-        local_map = wl.coef[0].reshape(H, W, k) if args.layout == "pixel" else wl.coef[0].reshape(k, H, W)
-        for _ in range(2):
-            gather_rows(local_map, H * world)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        g0 = time.perf_counter()
-        for _ in range(5):
-            gather_rows(local_map, H * world)
-        torch.cuda.synchronize(dev)
-        gather_ms = (time.perf_counter() - g0) / 5 * 1e3
-        # end to end: the row-chunked fit with each chunk's all-gather overlapped with the next fit
-        from rti.parallel import fit_rowtiled_overlapped
-
-        Irows = wl.I[0].reshape(wl.N, H, W)
-        for _ in range(2):
-            fit_rowtiled_overlapped(Irows, wl.lu, wl.lv, H * world, basis=wl.basis, chunks=4)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        g0 = time.perf_counter()
-        for _ in range(5):
-            fit_rowtiled_overlapped(Irows, wl.lu, wl.lv, H * world, basis=wl.basis, chunks=4)
-        torch.cuda.synchronize(dev)
-        e2e_ms = (time.perf_counter() - g0) / 5 * 1e3
-
-    value = world * wl.units * args.steps / elapsed / 1e6
-    achieved = wl.alg_bytes / (kernel_ms * 1e-3) / 1e9
-    workload_key = f"{args.config}-{args.kernel}-{args.layout}" + ("" if args.in_dtype == "f32" else f"-{args.in_dtype}")
+    value = wl.total_units * args.steps / elapsed / 1e6
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = wl.cpu_baseline(args.cpu_budget)
+        cpu = cpu_baseline(wl, args.cpu_budget)
     if rank == 0:
-        conf = {"workload": wl.desc, "H_per_rank": wl.H, "W": wl.W}
+        conf = {"workload": wl.desc, "H": ctx.H, "W": wl.W, "H_per_rank": ctx.h}
         conf.update(wl.config())
-        conf["parallelism"] = f"row-stripes x{world} (one {wl.H}-row stripe per GPU)"
+        conf["parallelism"] = (f"row-tiled x{world}: rank r fits rows [r*H/G, (r+1)*H/G) of one {ctx.H}-row image"
+                               if not args.weak else f"row-tiled x{world}: one {ctx.h}-row image per GPU (weak)")
         line = {
             "metric": wl.metric,
             "value": round(value, 1),
@@ -617,23 +999,23 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
-            "dtype": {"perpixel": "f32 in / f64 solve", "operator": ("f32 operator as 2 x f16 (f16 MFMA, f32 accumulate) -> int32"
-                                                       if args.op_precision == "split16" else "f32 (MFMA) -> int32"),
-                      "rbf_perpixel": "f64 -> int32", "frame": "f32 eval -> u8 BGR"}.get(kind, "f32" if args.in_dtype == "f32"
-                                                          else f"{args.in_dtype} in / f32 compute"),
+            "dtype": wl.dtype,
             "data": "synthetic (seeded smooth PTM/HSH coefficient fields + N(0,2) noise, rounded to 0..255, fp32)",
             "config": conf,
-            "roofline": wl.roofline(kernel_ms) if hasattr(wl, "roofline") else {
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(workload_key),
-                "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": wl.alg_bytes},
+            "roofline": wl.roofline(kernel_ms),
+            "kernel_ms_stats": {"median": round(float(np.median(kms)), 5), "min": round(float(kms.min()), 5),
+                                "mean": round(float(kms.mean()), 5), "n": int(kms.size), "warmup": 10,
+                                "per_rank_median": [round(x, 5) for x in kernel_ms_rank]},
+            "parity": parity,
             "cpu_baseline": cpu,
         }
         if gather_ms is not None:
             line["allgather_ms"] = round(gather_ms, 3)
-            line["fit_allgather_overlapped_ms"] = round(e2e_ms, 3)  # 4 row chunks, gather(c) || fit(c+1)
+            line["fit_allgather_overlapped_ms"] = round(e2e_ms, 3)  # row chunks, gather(c) || fit(c+1)
+            line["overlap_chunks"] = int(n_chunks)
+            line["end_to_end_Mpix_lights_per_s"] = round(wl.total_units / (e2e_ms * 1e-3) / 1e6, 1)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -102,6 +102,10 @@ int         rti_device_count(void);            /* hipGetDeviceCount, 0 on failur
 int rti_design_matrix(int basis, const float* lu, const float* lv, int n, double* A);
 int rti_pinv(int basis, const float* lu, const float* lv, int n, double rcond, double* pinv);
 int rti_basis_eval(int basis, const double* lu, const double* lv, int E, double* out);
+/* rti_gram_inverse: the Gram (pseudo-)inverse ginv[k][k] = (AᵀA)⁺ = V Σ⁻² Vᵀ of the same shared
+ * design and SVD as rti_pinv (so pinv = ginv·Aᵀ; rcond as there), the operator with which
+ * rti_fit_shared_residual turns Aᵀ I into coefficients (analysis.py:293-298). */
+int rti_gram_inverse(int basis, const float* lu, const float* lv, int n, double rcond, double* ginv);
 
 /* ---- device: shared-direction fit (the north_star hot path) ------------------------
  * Replaces interpolate_intensities' per-pixel loop + _interpolate_PTM's solve
@@ -133,6 +137,23 @@ int64_t rti_fit_residual_blocks(int64_t P);
 int rti_fit_residual(const float* A, int k, int N, const void* I, int in_dtype, int64_t P, int C,
                      int64_t light_stride, int64_t channel_stride, const float* coef, int coef_layout,
                      int64_t coef_channel_stride, float* res, double* partial, rti_stream_t stream);
+
+/* ---- device: shared-direction fit + residuals in ONE pass over the stack ---------------
+ * The north_star's fit with per-pixel residuals from wavefront reductions, reading the stack once
+ * (analysis.py:280-298 is the solve; its residual is never reported by the reference):
+ *   b = Aᵀ I[c][·][p], q = ‖I[c][·][p]‖²      accumulated in fp64 (exact fp32×fp32 products)
+ *   coef[c][p] = ginv · b                      (fp32 out, layout coef_layout, as rti_fit_shared)
+ *   ss = q − coefᵀ b,  res[c][p] = sqrt(ss/N), partial[c][blk] = Σ_workgroup ss (fp64)
+ * A: device fp64 design matrix [N][k] (rti_design_matrix); ginv: device fp64 [k][k]
+ * (rti_gram_inverse); k ∈ {6, 9, 16}.  I / strides / coef as rti_fit_shared.  res: NULL or device
+ * fp32 [C][P]; partial: NULL or device fp64 [C][rti_fit_shared_residual_blocks(P)] the caller zeroes.
+ * kernel: RTI_KERNEL_CHUNKS(n) overrides the chunks per lane (0 = AUTO); other bits ignored.
+ * 4 + 4(k+1)/N bytes per pixel·light (one stack read + coefficients + residual map). */
+int64_t rti_fit_shared_residual_blocks(int64_t P);
+int rti_fit_shared_residual(const double* A, const double* ginv, int k, int N, const void* I, int in_dtype,
+                            int64_t P, int C, int64_t light_stride, int64_t channel_stride,
+                            float* coef, int coef_layout, int64_t coef_channel_stride,
+                            float* res, double* partial, int kernel, rti_stream_t stream);
 
 /* ---- device: per-pixel PTM fit, light vectors generated in-kernel ------------------
  * Fuses compute_intensities' light vectors (analysis.py:221-231) into the

@@ -55,8 +55,9 @@ static void design_row(int basis, float lu, float lv, double* row) {
 }
 
 // One-sided (Hestenes) Jacobi SVD of A[n][k] (row-major, n >= k) and
-// pinv[k][n] = V Σ⁻¹ Uᵀ = Σ_m v_m (A v_m)ᵀ / σ_m².
-static void jacobi_pinv(const double* A, int n, int k, double rcond, double* pinv) {
+// pinv[k][n] = V Σ⁻¹ Uᵀ = Σ_m v_m (A v_m)ᵀ / σ_m²; optionally the Gram (pseudo-)inverse
+// ginv[k][k] = (AᵀA)⁺ = V Σ⁻² Vᵀ, so that pinv = ginv · Aᵀ.
+static void jacobi_pinv(const double* A, int n, int k, double rcond, double* pinv, double* ginv = nullptr) {
   std::vector<double> U(A, A + (size_t)n * k);  // column j = U[i*k + j]; becomes U·Σ
   std::vector<double> V((size_t)k * k, 0.0);
   for (int j = 0; j < k; ++j) V[(size_t)j * k + j] = 1.0;
@@ -113,15 +114,26 @@ static void jacobi_pinv(const double* A, int n, int k, double rcond, double* pin
     else
       inv2[m] = 1.0 / sig2[m];  // reference semantics: σ = 0 -> inf -> NaN entries
   }
-  for (int j = 0; j < k; ++j)
-    for (int i = 0; i < n; ++i) {
-      double acc = 0.0;
-      for (int m = 0; m < k; ++m) {
-        if (inv2[m] == 0.0) continue;
-        acc += V[(size_t)j * k + m] * (U[(size_t)i * k + m] * inv2[m]);
+  if (pinv)
+    for (int j = 0; j < k; ++j)
+      for (int i = 0; i < n; ++i) {
+        double acc = 0.0;
+        for (int m = 0; m < k; ++m) {
+          if (inv2[m] == 0.0) continue;
+          acc += V[(size_t)j * k + m] * (U[(size_t)i * k + m] * inv2[m]);
+        }
+        pinv[(size_t)j * n + i] = acc;
       }
-      pinv[(size_t)j * n + i] = acc;
-    }
+  if (ginv)
+    for (int j = 0; j < k; ++j)
+      for (int l = 0; l < k; ++l) {
+        double acc = 0.0;
+        for (int m = 0; m < k; ++m) {
+          if (inv2[m] == 0.0) continue;
+          acc += V[(size_t)j * k + m] * (V[(size_t)l * k + m] * inv2[m]);
+        }
+        ginv[(size_t)j * k + l] = acc;
+      }
 }
 
 // LU factorisation with partial pivoting (LAPACK getrf semantics), in place, row-major n×n.
@@ -218,6 +230,19 @@ int rti_pinv(int basis, const float* lu, const float* lv, int n, double rcond, d
   std::vector<double> A((size_t)n * k);
   for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], A.data() + (size_t)i * k);
   jacobi_pinv(A.data(), n, k, rcond, pinv);
+  return RTI_OK;
+}
+
+int rti_gram_inverse(int basis, const float* lu, const float* lv, int n, double rcond, double* ginv) {
+  const int k = basis_terms(basis);
+  if (k < 0) return fail(RTI_ERR_BAD_ARG, "rti_gram_inverse: unknown basis %d", basis);
+  if (!lu || !lv || !ginv || n <= 0) return fail(RTI_ERR_BAD_ARG, "rti_gram_inverse: null pointer or n <= 0");
+  if (n < k)
+    return fail(RTI_ERR_BAD_ARG, "rti_gram_inverse: %d lights < %d basis terms (shapes not aligned, analysis.py:298)",
+                n, k);
+  std::vector<double> A((size_t)n * k);
+  for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], &A[(size_t)i * k]);
+  jacobi_pinv(A.data(), n, k, rcond, nullptr, ginv);
   return RTI_OK;
 }
 

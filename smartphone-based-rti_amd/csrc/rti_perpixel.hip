@@ -181,10 +181,14 @@ fit_perpixel_dirs(const float* __restrict__ lu, const float* __restrict__ lv, co
 }
 
 // compute_intensities' light vectors (analysis.py:225-231); lane = (pixel, camera),
-// camera fastest so the pixel-major [P][N] stores are contiguous.
+// camera fastest so the pixel-major [P][N] stores are contiguous.  Every operation is a
+// separately rounded IEEE fp64 op in the order (dx² + dy²) + dz², sqrt, divide — no FMA
+// contraction — so the fp32 results are bit-identical to the reference's arrays (pinned by
+// tests/golden/ptm_perpixel_32x32_N50.npz).
 __global__ void __launch_bounds__(256)
 light_dirs(const double* __restrict__ cams, int N, int W, int64_t total, double x0, double y0,
            float* __restrict__ lu, float* __restrict__ lv) {
+#pragma clang fp contract(off)
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int n = (int)(i % N);

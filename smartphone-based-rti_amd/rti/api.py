@@ -86,6 +86,20 @@ def pinv(lu, lv, basis="ptm", rcond=None):
     return out
 
 
+def gram_inverse(lu, lv, basis="ptm", rcond=None):
+    """Host fp64 Gram (pseudo-)inverse (AᵀA)⁺ [k, k] of the shared design (pinv = ginv·Aᵀ; the
+    same SVD and rcond semantics as ``pinv``)."""
+    lu, lv = _f32_host(lu, "lu"), _f32_host(lv, "lv")
+    if lu.size != lv.size:
+        raise ValueError("lu and lv differ in length")
+    b = basis_id(basis)
+    k = basis_terms(b)
+    out = np.empty((k, k), dtype=np.float64)
+    rc = -1.0 if rcond is None else float(rcond)
+    L.check(L.lib().rti_gram_inverse(b, _fptr(lu), _fptr(lv), lu.size, rc, _dptr(out)), "rti_gram_inverse")
+    return out
+
+
 def basis_eval(lu, lv, basis="ptm"):
     """Host fp64 basis values [E, k] at (lu, lv)."""
     lu = np.ascontiguousarray(np.asarray(lu, np.float64).ravel())
@@ -266,6 +280,58 @@ def fit_residual(I, coef, lu, lv, basis="ptm", *, layout="pixel"):
     rms = torch.sqrt(partial.sum(dim=1) / (P * N))
     res = res.reshape((C,) + spatial)
     return (res, rms) if I.dim() == 4 else (res[0], rms[0])
+
+
+def _stack_shape(I):
+    if I.dim() == 2:
+        (N, P), C, spatial = I.shape, 1, (I.shape[1],)
+    elif I.dim() == 3:
+        N, H, W = I.shape
+        C, P, spatial = 1, H * W, (H, W)
+    elif I.dim() == 4:
+        C, N, H, W = I.shape
+        P, spatial = H * W, (H, W)
+    else:
+        raise ValueError("I must be [N, P], [N, H, W] or [C, N, H, W]")
+    return C, N, P, spatial
+
+
+def fit_with_residual(I, lu, lv, basis="ptm", rcond=None, *, layout="pixel", chunks=0):
+    """Shared-direction fit AND per-pixel residuals in ONE pass over the stack
+    (``rti_fit_shared_residual``; fp64 accumulation of Aᵀ I and ‖I‖², coefficients = (AᵀA)⁺ Aᵀ I).
+
+    I: CUDA [N, P], [N, H, W] or [C, N, H, W] (light-major, fp32/u8/int32).  Returns
+    ``(coef, res, rms)``: coef fp32 as ``fit`` returns it (layout), res fp32 with I's spatial shape
+    (leading C for 4-D stacks) = sqrt(Σ_n (I_n − A_n·coef)² / N) for the least-squares solution, and
+    rms fp64 [C] (0-d for 2/3-D stacks) = the RMS residual over all pixels, summed from per-workgroup
+    wavefront reductions."""
+    _require_cuda(I, "I")
+    if I.dtype not in _IN_DTYPES:
+        raise ValueError(f"I dtype {I.dtype} unsupported (float32, uint8 or int32)")
+    cl = _layout_id(layout)
+    b = basis_id(basis)
+    k = basis_terms(b)
+    C, N, P, spatial = _stack_shape(I)
+    if N < k:
+        raise ValueError(f"shapes not aligned: {N} lights < {k} basis terms (analysis.py:298)")
+    A = design_matrix(lu, lv, b)
+    if A.shape[0] != N:
+        raise ValueError(f"{A.shape[0]} light directions for {N} intensity planes")
+    dev = I.device
+    A_dev = torch.as_tensor(A, device=dev).contiguous()
+    G_dev = torch.as_tensor(gram_inverse(lu, lv, b, rcond), device=dev).contiguous()
+    Ic = I.contiguous().reshape(C, N, P)
+    coef = torch.empty((C, P, k) if cl == L.RTI_COEF_PIXEL_MAJOR else (C, k, P), dtype=torch.float32, device=dev)
+    res = torch.empty((C, P), dtype=torch.float32, device=dev)
+    partial = torch.zeros((C, int(L.lib().rti_fit_shared_residual_blocks(P))), dtype=torch.float64, device=dev)
+    st = L.lib().rti_fit_shared_residual(_vp(A_dev), _vp(G_dev), k, N, _vp(Ic), _IN_DTYPES[Ic.dtype], P, C, P, N * P,
+                                         _vp(coef), cl, P * k, _vp(res), _vp(partial),
+                                         int(chunks) << L.RTI_KERNEL_CHUNKS_SHIFT, _stream_of(I))
+    L.check(st, "rti_fit_shared_residual")
+    rms = torch.sqrt(partial.sum(dim=1) / (P * N))
+    coef = coef.reshape((C,) + spatial + (k,)) if cl == L.RTI_COEF_PIXEL_MAJOR else coef.reshape((C, k) + spatial)
+    res = res.reshape((C,) + spatial)
+    return (coef, res, rms) if I.dim() == 4 else (coef[0], res[0], rms[0])
 
 
 def light_dirs(cams, H, W, origin=(0.0, 0.0), device="cuda"):

@@ -12,6 +12,19 @@ from . import _lib as L
 from . import api
 
 
+def _same_device(**tensors):
+    """Every tensor on one device: a pointer from another GPU must not reach a kernel launched
+    on this GPU's stream."""
+    devs = {name: t.device for name, t in tensors.items()}
+    if len(set(devs.values())) > 1:
+        raise ValueError("tensors on different devices: " + ", ".join(f"{n}={d}" for n, d in devs.items()))
+
+
+def _in_dtype(I):
+    if I.dtype not in api._IN_DTYPES:
+        raise ValueError(f"I dtype {I.dtype} unsupported (float32, uint8 or int32)")
+
+
 @torch.library.custom_op("rti::fit_shared", mutates_args=())
 def fit_shared(pinv: torch.Tensor, I: torch.Tensor, planar: bool = False, kernel: int = 0) -> torch.Tensor:
     """coef = pinv (fp32 [k, N]) applied to I (CUDA [N, P] or [C, N, P]) -> [C?, P, k] or [C?, k, P]."""
@@ -19,6 +32,8 @@ def fit_shared(pinv: torch.Tensor, I: torch.Tensor, planar: bool = False, kernel
     api._require_cuda(pinv, "pinv")
     if pinv.dtype != torch.float32:
         raise ValueError("pinv must be float32")
+    _same_device(pinv=pinv, I=I)
+    _in_dtype(I)
     k = pinv.shape[0]
     I3 = I.contiguous() if I.dim() == 3 else I.contiguous().unsqueeze(0)
     C, N, P = I3.shape
@@ -49,6 +64,8 @@ def fit_residual(A: torch.Tensor, I: torch.Tensor, coef: torch.Tensor) -> torch.
     api._require_cuda(coef, "coef")
     if A.dtype != torch.float32 or coef.dtype != torch.float32:
         raise ValueError("A and coef must be float32")
+    _same_device(A=A, I=I, coef=coef)
+    _in_dtype(I)
     if I.dim() != 2:
         raise ValueError("I must be [N, P]")
     N, P = I.shape

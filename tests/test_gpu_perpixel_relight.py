@@ -17,10 +17,8 @@ def test_light_dirs_match_reference(cuda):
     d = golden("ptm_perpixel_32x32_N50.npz")
     lu, lv = rti.light_dirs(d["cams"], 32, 32, device=cuda)
     lu, lv = lu.cpu().numpy(), lv.cpu().numpy()
-    # same fp64 formula rounded to fp32; allow 1 ulp for the reference's BLAS dot in np.linalg.norm
-    assert np.abs(lu - d["lx"]).max() <= np.finfo(np.float32).eps
-    assert np.abs(lv - d["ly"]).max() <= np.finfo(np.float32).eps
-    assert (lu == d["lx"]).mean() > 0.999
+    # separately rounded fp64 ops (no contraction) rounded to fp32: bit-identical to the reference
+    assert np.array_equal(lu, d["lx"]) and np.array_equal(lv, d["ly"])
 
 
 @pytest.mark.parametrize("coef_dtype", [torch.float64, torch.float32])
@@ -123,7 +121,7 @@ def test_compat_compute_intensities(cuda):
     data = [(d["frames"][i], d["cams"][i]) for i in range(len(d["cams"]))]
     lx, ly, inten = compat.compute_intensities(data)
     assert lx.dtype == np.float32 and inten.dtype == np.int32 and lx.shape == (32, 32, 50)
-    assert np.abs(lx - d["lx"]).max() <= np.finfo(np.float32).eps
+    assert np.array_equal(lx, d["lx"]) and np.array_equal(ly, d["ly"])
     assert np.array_equal(inten, d["I"])
     with pytest.raises(Exception, match="results are empty"):
         compat.compute_intensities([])
@@ -140,9 +138,15 @@ def test_compat_interpolate_and_prepare(cuda):
     tables = compat.prepare_images_data(grid)
     ref_t = d["tables"]
     # int32 truncation can only differ where the reference value sits within 1e-4 of an integer
+    # (fp64 Cholesky normal equations vs the reference's SVD: coefficients agree to ~4e-8
+    # relative).  The flips are counted and reported, not only bounded.
     diff = tables != ref_t
     near = np.abs(np.transpose(d["grid"], (2, 3, 0, 1)) - np.round(np.transpose(d["grid"], (2, 3, 0, 1)))) < 1e-4
+    flips = int(diff.sum())
+    print(f"per-pixel PTM int32 tables: {flips} of {diff.size} entries differ from the reference "
+          f"({int(near.sum())} reference values lie within 1e-4 of an integer)")
     assert not (diff & ~near).any()
+    assert flips <= int(near.sum()) and flips / diff.size < 1e-4
     assert np.array_equal(compat.prepare_images_data(d["grid"]), ref_t)
     one = compat.interpolate_intensities(data, interpolate_PTM=True, first_only=True)
     assert one.shape == (1, 1, 100, 100)
@@ -197,4 +201,7 @@ def test_compat_compute_end_to_end(cuda, tmp_path, ptm):
         r = golden("rbf_perpixel_4x4_N50.npz")
         ref_grid, ref_t = r["grid"], r["tables"]
     near = np.abs(ref_grid - np.round(ref_grid)) < 1e-4
-    assert not ((tables != ref_t) & ~np.transpose(near, (2, 3, 0, 1))).any()
+    diff = tables != ref_t
+    print(f"compute({'PTM' if ptm else 'RBF'}) tables: {int(diff.sum())} of {diff.size} entries differ "
+          f"from the reference")
+    assert not (diff & ~np.transpose(near, (2, 3, 0, 1))).any()

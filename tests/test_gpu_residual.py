@@ -126,3 +126,28 @@ def test_custom_op_matches_api(cuda):
     N = I.shape[0]
     got = torch.ops.rti.fit_residual(A, I.reshape(N, -1), coef.reshape(-1, 6))
     assert torch.equal(got, res.reshape(-1))
+
+
+@pytest.mark.parametrize("layout", ["pixel", "planar"])
+@pytest.mark.parametrize("in_dtype", [torch.float32, torch.uint8])
+def test_wide_lane_path_ragged(cuda, layout, in_dtype):
+    """The PTM-6 4-chunks-per-lane residual path (taken when P·C >= 2.048 M) with a ragged pixel
+    count (P % 4096 != 0: a partial last wave whose lanes hold only some chunks), 3 channels,
+    both coefficient layouts, 8-bit and fp32 stacks — per pixel against the oracle."""
+    n, C, P = 12, 3, 700001 * 4
+    lu, lv = o.synth_dirs(n, 41)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    I = torch.randint(0, 256, (C, n, P), generator=g, device=cuda).to(in_dtype)
+    coef = rti.fit(I.reshape(C, n, P // 4, 4), lu, lv, layout=layout)
+    res, rms = rti.fit_residual(I.reshape(C, n, P // 4, 4), coef, lu, lv, layout=layout)
+    A = o.design("ptm", lu, lv)
+    idx = np.concatenate([np.arange(4096), np.arange(P - 8192, P)])  # the start and the ragged tail
+    for c in range(C):
+        cc = coef[c].reshape(P, 6) if layout == "pixel" else coef[c].reshape(6, P).T
+        Ic = I[c][:, idx].double().cpu().numpy()
+        ref, _ = o.fit_residual(Ic, A, cc[idx].cpu().numpy())
+        got = res[c].reshape(P)[idx].cpu().numpy()
+        assert np.all(np.abs(got - ref) <= 1e-3 + 1e-4 * ref), (c, np.abs(got - ref).max())
+        _, ss = o.fit_residual(I[c].double().cpu().numpy(), A, cc.cpu().numpy())
+        ref_rms = np.sqrt(ss / (n * P))
+        assert abs(float(rms[c]) - ref_rms) <= 1e-4 * ref_rms + 1e-3, (c, float(rms[c]), ref_rms)

@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from rti.parallel import gather_rows, gather_rows_pipelined, row_range
+from rti.parallel import cyclic_rows, gather_rows, gather_rows_pipelined, row_range
 
 
 def _free_port():
@@ -103,3 +103,82 @@ def test_gather_rows_pipelined(H, W, chunks, world):
         assert p.exitcode == 0
     for rank, ok, covered in results:
         assert ok and covered, rank
+
+
+@pytest.mark.parametrize("H,world,chunks", [(2160, 8, 3), (2160, 4, 4), (40, 2, 4), (12, 3, 2)])
+def test_cyclic_rows_partition(H, world, chunks):
+    blocks = [b for r in range(world) for b in cyclic_rows(H, world, r, chunks)]
+    assert sorted(blocks) == [(i * H // (world * chunks), (i + 1) * H // (world * chunks))
+                              for i in range(world * chunks)]
+    # chunk c of all ranks is one contiguous row range, rank-major: the in-place gather target
+    for c in range(chunks):
+        rows = [cyclic_rows(H, world, r, chunks)[c] for r in range(world)]
+        assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
+    with pytest.raises(ValueError):
+        cyclic_rows(H + 1, world, 0, chunks)
+
+
+def _cyclic_worker(rank, world, port, H, W, chunks, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full_ref = torch.arange(H * W * 6, dtype=torch.float32).reshape(H, W, 6)
+        local = torch.cat([full_ref[a:b] for a, b in cyclic_rows(H, world, rank, chunks)])
+
+        def produce(c0, c1):
+            return local[c0:c1].clone()
+
+        out = torch.full((H, W, 6), -1.0)
+        full = gather_rows_pipelined(produce, local.shape[0], H, (W, 6), torch.float32, torch.device("cpu"),
+                                     chunks=chunks, partition="cyclic", out=out)
+        q.put((rank, bool(torch.equal(full, full_ref)) and full is out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("H,W,chunks,world", [(16, 3, 4, 2), (12, 2, 2, 3)])
+def test_gather_rows_pipelined_cyclic(H, W, chunks, world):
+    """Block-cyclic rows: every chunk's all-gather lands in place in the caller's map."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cyclic_worker, args=(r, world, port, H, W, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok in results:
+        assert ok, rank
+
+
+def _bench_plan(args):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("gpus", [2, 4])
+def test_bench_spawns_ranks_strong_scaling(gpus):
+    """bench.py --gpus N re-launches itself under torch.distributed.run with N ranks; by default each
+    rank gets H/N rows of the same image (strong scaling)."""
+    line = _bench_plan(["--gpus", str(gpus), "--plan", "--config", "c3"])
+    assert line["n_gpus"] == gpus and line["scaling"] == "strong"
+    assert line["config"]["H"] == 2160 and line["config"]["H_per_rank"] == 2160 // gpus
+    assert line["config"]["rows_per_rank"] == [[r * 2160 // gpus, (r + 1) * 2160 // gpus] for r in range(gpus)]
+
+
+def test_bench_weak_option():
+    line = _bench_plan(["--gpus", "2", "--plan", "--weak"])
+    assert line["scaling"] == "weak" and line["config"]["H_per_rank"] == 2160 and line["config"]["H"] == 4320

@@ -32,9 +32,11 @@ def main():
                     "valu:planar:nt,valu:planar:nt+nts,valu:planar:nt+lds+nts,valu:planar:nt+lds,"
                     "mfma:planar:nt,mfma:pixel:nt")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--rows", type=int, default=0, help="override the config's H (row-shard sizes: 2160/G)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     _, H, W, N, C, basis, desc = bench.CONFIGS[args.config]
+    H = args.rows or H
     k = rti.basis_terms(basis)
     P = H * W
     lu, lv = bench.synth_dirs(N, 2)

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Interleaved A/B (one process, HIP events around each launch) of the one-pass fit + residual
+kernel (rti_fit_shared_residual) at every chunks-per-lane setting against the two-pass form
+(rti_fit_shared + rti_fit_residual) and the fit alone, on a bench.py config.
+
+  python tools/sweep_fitres.py [--config c3] [--rows H] [--rounds 30]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "smartphone-based-rti_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import rti  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--rounds", type=int, default=30)
+    ap.add_argument("--chunks", default="1,2,3,4")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    _, H, W, N, C, basis, desc = bench.CONFIGS[args.config]
+    H = args.rows or H
+    k = rti.basis_terms(basis)
+    P = H * W
+    L = rti._lib
+    lib = L.lib()
+    lu, lv = bench.synth_dirs(N, 2)
+    I = bench.synth_stack(H, W, N, C, basis, lu, lv, 1000, dev)
+    A64 = torch.as_tensor(rti.design_matrix(lu, lv, basis), device=dev)
+    A32 = A64.float().contiguous()
+    G = torch.as_tensor(rti.gram_inverse(lu, lv, basis), device=dev)
+    pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=dev)
+    coef = torch.empty((C, P, k), device=dev)
+    res = torch.empty((C, P), device=dev)
+    nb = int(lib.rti_fit_shared_residual_blocks(P))
+    part = torch.zeros((C, max(nb, int(lib.rti_fit_residual_blocks(P)))), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    s = ctypes.c_void_p(stream.cuda_stream)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def fused(nc):
+        return lambda: L.check(lib.rti_fit_shared_residual(vp(A64), vp(G), k, N, vp(I), L.RTI_F32, P, C, P, N * P,
+                                                           vp(coef), L.RTI_COEF_PIXEL_MAJOR, P * k, vp(res), vp(part),
+                                                           nc << L.RTI_KERNEL_CHUNKS_SHIFT, s), "fused")
+
+    def fit():
+        L.check(lib.rti_fit_shared(vp(pv), k, N, vp(I), L.RTI_F32, P, C, P, N * P, vp(coef), L.RTI_COEF_PIXEL_MAJOR,
+                                   P * k, 0, s), "fit")
+
+    def resid():
+        L.check(lib.rti_fit_residual(vp(A32), k, N, vp(I), L.RTI_F32, P, C, P, N * P, vp(coef), L.RTI_COEF_PIXEL_MAJOR,
+                                     P * k, vp(res), vp(part), s), "resid")
+
+    variants = [(f"fused_nc{nc}", fused(nc)) for nc in map(int, args.chunks.split(","))]
+    variants += [("fit_only", fit), ("residual_only", resid)]
+    for _, fn in variants:
+        for _ in range(3):
+            fn()
+    torch.cuda.synchronize()
+    times = {n: [] for n, _ in variants}
+    for _ in range(args.rounds):
+        for name, fn in variants:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fn()
+            b.record(stream)
+            times[name].append((a, b))
+    torch.cuda.synchronize()
+    alg = 4.0 * P * N * C + 4.0 * P * (k + 1) * C
+    out = {}
+    for name, _ in variants:
+        ms = np.array([a.elapsed_time(b) for a, b in times[name]])
+        out[name] = {"median_ms": float(np.median(ms)), "min_ms": float(ms.min())}
+        gbs = alg / (np.median(ms) * 1e-3) / 1e9
+        print(f"{name:16s} median {np.median(ms):.4f} ms  min {ms.min():.4f} ms  {gbs:.0f} GB/s of one-pass bytes "
+              f"({gbs / 80:.1f}% of 8 TB/s)", flush=True)
+    two = out["fit_only"]["median_ms"] + out["residual_only"]["median_ms"]
+    print(f"two-pass (fit + residual) {two:.4f} ms")
+    print(json.dumps({"config": args.config, "rows": H, "results": out, "two_pass_ms": two}))
+
+
+if __name__ == "__main__":
+    main()
