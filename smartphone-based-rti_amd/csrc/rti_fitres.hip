@@ -282,8 +282,9 @@ int launch_fr_k(const FrArgs& a, bool vec4) {
   }
 }
 
-// AUTO chunks per lane: see DESIGN.md §4.1b (profiles/r02_fitres_*): the widest run whose fp64
-// accumulators still leave >= 2 waves per SIMD, while the launch keeps >= 2000 waves.
+// AUTO chunks per lane (profiles/r02_fitres_c3_sweep.log, c3 4K x 100 PTM-6: 1 / 2 / 3 / 4 chunks
+// -> 0.618 / 0.603 / 0.598 / 0.718 ms; 4 chunks need 256 VGPRs = 1 wave per SIMD): 3 for PTM-6 while
+// the launch keeps >= 2000 waves, else 2 or 1; HSH-9/16 one (their fp64 state fills the registers).
 constexpr int64_t FR_MIN_WAVES = 2000;
 
 }  // namespace
@@ -334,7 +335,7 @@ extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int 
   if (a.nc == 0) {
     a.nc = 1;
     if (k == 6)
-      for (int nc = 2; nc > 1; nc >>= 1)
+      for (int nc = 3; nc > 1; --nc)
         if (P * C / (64 * 4 * nc) >= FR_MIN_WAVES) {
           a.nc = nc;
           break;

@@ -62,7 +62,7 @@ def test_chunks_ragged(cuda, chunks, basis, n, in_dtype):
     for P in (3, 4, wave_px - 4, wave_px + 4, 3 * wave_px + 260, 5 * wave_px + 1024 * 3 + 8, 4099):
         rng = np.random.default_rng(P + n)
         I = rng.integers(0, 256, size=(2, n, P)).astype(np.float32)
-        Id = torch.as_tensor(I, device=cuda).to(in_dtype)
+        Id = torch.as_tensor(I, device=cuda).to(in_dtype)[..., None]  # [C, N, P, 1]
         for layout in ("pixel", "planar"):
             coef, res, rms = rti.fit_with_residual(Id, lu, lv, basis=basis, layout=layout, chunks=chunks)
             for c in range(2):
