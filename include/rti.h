@@ -79,6 +79,10 @@ extern "C" {
  * 3 or 4 = global_load_lds ring with depth-1 steps in flight (fp32 stacks) */
 #define RTI_KERNEL_TILE_DEPTH_SHIFT 20
 #define RTI_KERNEL_TILE_DEPTH(n)    ((n) << RTI_KERNEL_TILE_DEPTH_SHIFT)
+/* TILE kernel, fp32 stacks: waves per workgroup (bits 24-27; 0 = 4).  8 = one light plane per wave
+ * and step with the plane loads issued DEPTH − 1 steps ahead in registers (DEPTH 2 or 3) */
+#define RTI_KERNEL_TILE_WAVES_SHIFT 24
+#define RTI_KERNEL_TILE_WAVES(n)    ((n) << RTI_KERNEL_TILE_WAVES_SHIFT)
 
 typedef void* rti_stream_t; /* hipStream_t */
 
@@ -232,7 +236,7 @@ int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp,
  * out: F64 / F32 / I32 / U8, layout RTI_OUT_PIXEL_MAJOR ([p][e], the reference's
  * [y][x][ly][lx]) or RTI_OUT_EVAL_MAJOR ([e][p], prepare_images_data's [ly][lx][y][x]).
  * status: device int the caller zeroes; set to RTI_ERR_SINGULAR when a pixel's system is
- * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 128. */
+ * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 256. */
 int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                      const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
                      rti_stream_t stream);

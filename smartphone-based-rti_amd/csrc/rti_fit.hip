@@ -428,6 +428,124 @@ fit_shared_tile(const float* __restrict__ pinv, int k, int N, const T* __restric
   tile_store<RC, LAYOUT>(acc, coef + (int64_t)blockIdx.y * ocstride, P, k, t0 + pw, q, r);
 }
 
+// Wide-workgroup form: W waves (512 threads at W = 8), ONE light plane per wave and step (S = W
+// planes), the same [2][S][R] double-buffered LDS tile, and the plane loads issued AHEAD steps
+// before they are parked in LDS (AHEAD = 2 keeps two steps of loads in flight in registers: the
+// register-staged kernel above has one, 64 KiB per CU).  Each wave computes R/W pixels of every
+// step (acc = 4·R/(64·W) floatx4: 64 VGPRs at R = 2048, W = 8), so the MFMA accumulators shrink
+// as the waves grow and the registers go to loads in flight instead.
+template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT>
+__global__ void __launch_bounds__(64 * W)
+fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P,
+                  int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  constexpr int R = 256 * RC, S = W, G = R / (64 * W);  // G = 64-pixel groups per wave
+  static_assert(G >= 1 && R % (64 * W) == 0, "tile must split into 64-pixel groups per wave");
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  const int T_ = (N + S - 1) / S;  // steps
+  float* __restrict__ lds_pinv = lds_dyn;             // [T_·S][16]
+  float* __restrict__ tile = lds_dyn + T_ * S * 16;  // [2][S][R]
+  for (int idx = threadIdx.x; idx < T_ * S * 16; idx += 64 * W) {
+    const int n = idx >> 4, i = idx & 15;
+    lds_pinv[idx] = (i < k && n < N) ? pinv[i * N + n] : 0.f;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * R;
+  const T* __restrict__ src = I + (int64_t)blockIdx.y * cstride + t0 + 4 * lane;
+  bool pin[RC];
+#pragma unroll
+  for (int c = 0; c < RC; ++c) pin[c] = t0 + 256 * c + 4 * lane < P;
+  auto load = [&](int t, floatx4 (&st)[RC]) {
+    const int n = t * S + wave;
+#pragma unroll
+    for (int c = 0; c < RC; ++c) {
+      float x[4] = {0.f, 0.f, 0.f, 0.f};
+      if (n < N && pin[c]) load_px<T, 4, NT>(src + (int64_t)n * lstride + 256 * c, x);
+      st[c] = floatx4{x[0], x[1], x[2], x[3]};
+    }
+  };
+  auto park = [&](int b, const floatx4 (&st)[RC]) {
+    float* __restrict__ tb = tile + b * (S * R) + wave * R;
+#pragma unroll
+    for (int c = 0; c < RC; ++c) *reinterpret_cast<floatx4*>(tb + 256 * c + 4 * lane) = st[c];
+  };
+  const int q = lane & 15, r = lane >> 4;
+  const int pw = wave * 64 * G;
+  floatx4 acc[G][4];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[g][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int b, int t) {
+    const float* __restrict__ tb = tile + b * (S * R);
+#pragma unroll
+    for (int s = 0; s < S / 4; ++s) {
+      const float a = lds_pinv[(t * S + 4 * s + r) * 16 + q];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const floatx4 x = *reinterpret_cast<const floatx4*>(tb + (4 * s + r) * R + pw + 64 * g + 4 * q);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[g][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[c], acc[g][c], 0, 0, 0);
+      }
+    }
+  };
+  floatx4 sa[RC], sb[RC];
+  load(0, sa);
+  if constexpr (AHEAD >= 2) {
+    if (T_ > 1) load(1, sb);
+  }
+  park(0, sa);
+  __syncthreads();
+  if constexpr (AHEAD == 1) {
+    for (int t = 0; t < T_; ++t) {
+      const bool more = t + 1 < T_;  // workgroup-uniform
+      if (more) load(t + 1, sa);
+      compute(t & 1, t);
+      if (more) park((t + 1) & 1, sa);
+      __syncthreads();
+    }
+  } else {
+    // sb holds step t + 1 (loaded during step t − 1), sa receives step t + 2; the roles swap every
+    // step, so the loop body is written for an even and an odd step
+    int t = 0;
+    for (; t + 1 < T_; t += 2) {
+      if (t + 2 < T_) load(t + 2, sa);
+      compute(0, t);
+      park(1, sb);
+      __syncthreads();
+      if (t + 3 < T_) load(t + 3, sb);
+      compute(1, t + 1);
+      if (t + 2 < T_) park(0, sa);
+      __syncthreads();
+    }
+    if (t < T_) compute(t & 1, t);  // odd step count: the last step, parked by the previous one
+  }
+  // acc[g][c][rr] = coefficient 4r + rr of pixel t0 + pw + 64g + 4q + c
+  float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t px = t0 + pw + 64 * g + 4 * q;
+    if (px >= P) continue;
+    if constexpr (LAYOUT == RTI_COEF_PLANAR) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = 4 * r + rr;
+        if (i < k)
+          *reinterpret_cast<floatx4*>(dst + (int64_t)i * P + px) =
+              floatx4{acc[g][0][rr], acc[g][1][rr], acc[g][2][rr], acc[g][3][rr]};
+      }
+    } else if (k == 16) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *reinterpret_cast<floatx4*>(dst + (px + c) * 16 + 4 * r) = acc[g][c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          if (4 * r + rr < k) dst[(px + c) * k + 4 * r + rr] = acc[g][c][rr];
+    }
+  }
+}
+
 // DMA form (fp32 stacks): the tile planes go HBM -> LDS by global_load_lds_dwordx4 (no VGPR
 // hop, 1 KiB per wave instruction) into a ring of NB tiles, NB - 1 steps in flight.  A step
 // waits for its own wave's DMAs with a counted vmcnt and one raw s_barrier publishes it to the
@@ -705,6 +823,38 @@ int launch_tile_l(const FitArgs& a) {
               : launch_tile_t<RC, SP, T, RTI_COEF_PIXEL_MAJOR, false>(a);
 }
 
+template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT>
+int launch_tile_w_t(const FitArgs& a) {
+  constexpr int R = 256 * RC, S = W;
+  const int T_ = (a.N + S - 1) / S;
+  const size_t lds = ((size_t)T_ * S * 16 + (size_t)2 * S * R) * sizeof(float);
+  if (lds > 160 * 1024)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
+  auto kern = fit_shared_tile_w<RC, W, AHEAD, T, LAYOUT, NT>;
+  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
+  dim3 grid(grid_1d(a.P, R), a.C);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * W), lds, a.stream, a.pinv, a.k, a.N, static_cast<const T*>(a.I), a.P,
+                     a.lstride, a.cstride, a.coef, a.ocstride);
+  return RTI_OK;
+}
+
+// wide-workgroup tile (fp32): rc 4 or 8, 8 waves, loads 1 or 2 steps ahead
+template <int RC, int AHEAD>
+int launch_tile_w_l(const FitArgs& a) {
+  if (a.layout == RTI_COEF_PLANAR)
+    return a.nt ? launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PLANAR, true>(a)
+                : launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PLANAR, false>(a);
+  return a.nt ? launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PIXEL_MAJOR, true>(a)
+              : launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PIXEL_MAJOR, false>(a);
+}
+
+int launch_tile_w(const FitArgs& a, int rc, int depth) {
+  if (rc >= 8) return depth >= 3 ? launch_tile_w_l<8, 2>(a) : launch_tile_w_l<8, 1>(a);
+  return depth >= 3 ? launch_tile_w_l<4, 2>(a) : launch_tile_w_l<4, 1>(a);
+}
+
 template <int RC, int SP, int NB, int LAYOUT, bool NT>
 int launch_tile_dma_t(const FitArgs& a) {
   constexpr int R = 256 * RC, S = 4 * SP;
@@ -741,8 +891,9 @@ int launch_tile_dma(const FitArgs& a, int rc, int sp) {
 // depth: tiles in the LDS ring (2 = register-staged double buffer; 3, 4 = DMA ring, fp32 only).
 // Every (rc, sp) for fp32 stacks; 8-bit and int32 stacks use the register-staged (4, 1).
 template <typename T>
-int launch_tile(const FitArgs& a, int rc, int sp, int depth) {
+int launch_tile(const FitArgs& a, int rc, int sp, int depth, int waves) {
   if constexpr (std::is_same<T, float>::value) {
+    if (waves == 8) return launch_tile_w(a, rc, depth);
     if (depth >= 4) return launch_tile_dma<4>(a, rc, sp);
     if (depth == 3) return launch_tile_dma<3>(a, rc, sp);
   }
@@ -861,12 +1012,13 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
       // where the 128 KiB double tile and the [N][16] pseudo-inverse no longer fit 160 KiB of LDS)
       const int rc = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, sp = (kernel >> RTI_KERNEL_TILE_PLANES_SHIFT) & 0xF;
       const int depth = (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF;
+      const int waves = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF;
       const int rc0 = rc ? rc : (N <= 512 ? 8 : 4);
       int st;
       switch (in_dtype) {
-        case RTI_F32: st = launch_tile<float>(a, rc0, sp ? sp : 2, depth ? depth : 2); break;
-        case RTI_I32: st = launch_tile<int32_t>(a, 4, 1, 2); break;
-        default: st = launch_tile<uint8_t>(a, 4, 1, 2); break;
+        case RTI_F32: st = launch_tile<float>(a, rc0, sp ? sp : 2, depth ? depth : 2, waves); break;
+        case RTI_I32: st = launch_tile<int32_t>(a, 4, 1, 2, 4); break;
+        default: st = launch_tile<uint8_t>(a, 4, 1, 2, 4); break;
       }
       return st != RTI_OK ? st : check_launch("rti_fit_shared");
     }

@@ -7,9 +7,10 @@
 // (LAPACK gesv: LU with partial pivoting) and evaluates f(q) = Σ_j w_j ‖q − x_j‖
 // on the 100×100 grid.  Every pixel has its own light list (compute_intensities,
 // analysis.py:225-231), so there is no shared operator: one workgroup owns one
-// pixel, factors its N×N system in LDS (fp32 factors + fp64 iterative refinement:
-// the systems reach cond ≈ 1e4–1e5 at N = 100–200) and streams the E evaluations,
-// one query per lane, in fp64.
+// pixel and solves its N×N system — fp64 Gauss-Jordan in registers up to N = 112, fp32 LU in LDS
+// + fp64 iterative refinement up to 128, Householder-projected fp32 Cholesky (packed triangle in
+// LDS) + fp64 refinement up to 256 (the systems reach cond ≈ 1e4–1e5 at N = 100–200) — and a
+// second kernel streams the E evaluations in fp64.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -21,7 +22,7 @@
 namespace rti {
 namespace {
 
-constexpr int RBF_MAX_N = 128;
+constexpr int RBF_MAX_N = 128;      // rbf_solve_lds (fp32 LU in LDS) up to here; Householder-Cholesky above
 constexpr int RBF_MAX_REFINE = 10;  // refinement sweeps of the fp32-LU fallback
 
 template <typename T>
@@ -293,6 +294,282 @@ rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const 
   }
 }
 
+// ---- 128 < N <= 256: Householder-projected Cholesky in LDS + fp64 refinement --------------
+// An fp32 LU of a 200×200 system no longer fits 160 KiB of LDS (and a 256×256 one is 256 KiB), but
+// the linear-RBF matrix A_ij = ‖x_i − x_j‖ of distinct nodes is symmetric and strictly
+// conditionally negative definite (negative definite on 1^⊥).  With the Householder reflector H
+// that maps e = 1/√N to the last unit vector, HAH = [M m; mᵀ μ] where M (order n = N − 1) is
+// Q̃ᵀAQ̃ on 1^⊥, so S = −M is symmetric positive definite: its fp32 Cholesky factor needs only the
+// packed lower triangle (n(n+1)/2 floats, 127.5 KiB at N = 256).  A w = b is then
+//   c = H b,  z1 = S⁻¹ c₁,  z2 = S⁻¹ m,  y_n = (c_n + mᵀz1)/(μ + mᵀz2),  y₁ = −z1 + z2·y_n,  w = H y
+// (block elimination of the bordered system), used as the approximate inverse of mixed-precision
+// iterative refinement exactly as rbf_solve_lds does: residuals b − A·w in fp64 from the node
+// coordinates, corrections through the fp32 factor, until the fp64 floor (cond·eps), so the result
+// is what SciPy's fp64 LU returns to rounding.  Exactly repeated nodes make A singular (SciPy's
+// LinAlgError): they are detected up front; a Cholesky pivot <= 0 (cond far beyond fp32) reports
+// the same status.
+constexpr int RBF_CH_MAX_N = 256;
+constexpr int RBF_CH_THREADS = 512;
+constexpr int RBF_CH_MAX_REFINE = 16;
+
+__device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower, j <= i
+
+__device__ __forceinline__ double pick4(const double (&v)[4], int q) {
+  return q == 0 ? v[0] : (q == 1 ? v[1] : (q == 2 ? v[2] : v[3]));
+}
+
+__device__ __forceinline__ double wave_sum64(double t) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+  return t;
+}
+
+// v ← S⁻¹ v for S = L Lᵀ (packed fp32 L of order n <= 256) on one wave: lane owns entries
+// lane + 64s; rd[s] = 1 / L_ii for the same entries.  Column-oriented forward then backward
+// substitution; the chain runs through registers (readlane), the next step's factor entries are
+// loaded before the current step's update.  Entries >= n are left unchanged.
+__device__ __forceinline__ void chol_solve(const float* __restrict__ L, int n, const double (&rd)[4], double (&v)[4],
+                                           int lane) {
+  float cur[4], nxt[4];
+  auto fwd_load = [&](int k, float (&dst)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) dst[s] = L[tri(max(min(lane + 64 * s, n - 1), k), k)];
+  };
+  fwd_load(0, cur);
+  for (int k = 0; k < n; ++k) {
+    if (k + 1 < n) fwd_load(k + 1, nxt);
+    const int q = k >> 6;
+    const double yk = readlane64(pick4(v, q), k & 63) * readlane64(pick4(rd, q), k & 63);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int i = lane + 64 * s;
+      if (i == k) v[s] = yk;
+      else if (i > k && i < n) v[s] = fma(-(double)cur[s], yk, v[s]);
+      cur[s] = nxt[s];
+    }
+  }
+  auto bwd_load = [&](int k, float (&dst)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) dst[s] = L[tri(k, min(lane + 64 * s, k))];
+  };
+  bwd_load(n - 1, cur);
+  for (int k = n - 1; k >= 0; --k) {
+    if (k > 0) bwd_load(k - 1, nxt);
+    const int q = k >> 6;
+    const double xk = readlane64(pick4(v, q), k & 63) * readlane64(pick4(rd, q), k & 63);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int i = lane + 64 * s;
+      if (i == k) v[s] = xk;
+      else if (i < k) v[s] = fma(-(double)cur[s], xk, v[s]);
+      cur[s] = nxt[s];
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(RBF_CH_THREADS)
+rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
+               double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int n = N - 1;
+  double* xs = smem;     // [N] nodes (fp64 copies of the fp32 light vectors)
+  double* ys = xs + N;   // [N]
+  double* b = ys + N;    // [N] right-hand side
+  double* w = b + N;     // [N] solution
+  double* v = w + N;     // [N] residual
+  double* g = v + N;     // [N] A·u
+  double* m = g + N;     // [N] (HAH)[·][n]; m[n] = μ
+  float* col = reinterpret_cast<float*>(m + N);  // [N] current Cholesky column
+  float* S = col + ((N + 3) & ~3);                // packed lower triangle of order n
+  __shared__ double s_red;
+  __shared__ int s_flag, s_more;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t p = blockIdx.x;
+  const int64_t base = p * N;
+
+  for (int j = tid; j < N; j += RBF_CH_THREADS) {
+    const float x = lu[base + j], y = lv[base + j];
+    xs[j] = (double)x;
+    ys[j] = (double)y;
+    b[j] = ldd(I + base + j);
+    xyT[(int64_t)j * P + p] = make_float2(x, y);
+  }
+  if (tid == 0) s_flag = 0;
+  __syncthreads();
+  // exactly repeated nodes: A has two equal rows (SciPy: LinAlgError)
+  for (int i = wave; i < N; i += RBF_CH_THREADS / 64)
+    for (int j = i + 1 + lane; j < N; j += 64)
+      if (xs[i] == xs[j] && ys[i] == ys[j]) s_flag = 1;
+  // Householder vector u = e − e_n (e = 1/√N), H = I − β u uᵀ, β = 2/uᵀu = 1/(1 − 1/√N)
+  const double e = 1.0 / sqrt((double)N), beta = 1.0 / (1.0 - e);
+  auto u = [&](int i) { return i < n ? e : e - 1.0; };
+  {  // g = A u, two threads per row
+    const int i = tid >> 1, h = tid & 1;
+    double r = 0.0;
+    if (i < N) {
+      const double xi = xs[i], yi = ys[i];
+      for (int j = h; j < N; j += 2) r = fma(dist64(xi, yi, xs[j], ys[j]), u(j), r);
+    }
+    r += __shfl_xor(r, 1);
+    if (i < N && h == 0) g[i] = r;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    double t = 0.0;
+    for (int j = lane; j < N; j += 64) t = fma(u(j), g[j], t);
+    t = wave_sum64(t);
+    if (lane == 0) s_red = t;
+  }
+  __syncthreads();
+  bool singular = s_flag != 0;  // block-uniform
+  if (!singular) {
+    const double sg = s_red, b2 = beta * beta * sg;
+    auto hah = [&](int i, int j) {
+      return dist64(xs[i], ys[i], xs[j], ys[j]) - beta * (u(i) * g[j] + g[i] * u(j)) + b2 * u(i) * u(j);
+    };
+    for (int i = wave; i < n; i += RBF_CH_THREADS / 64)
+      for (int j = lane; j <= i; j += 64) S[tri(i, j)] = (float)(-hah(i, j));
+    for (int i = tid; i < N; i += RBF_CH_THREADS) m[i] = hah(i, n);
+    __syncthreads();
+    // right-looking Cholesky of S: column k scaled, then the trailing triangle updated
+    for (int k = 0; k < n; ++k) {
+      const float dkk = S[tri(k, k)];
+      if (!(dkk > 0.f)) {  // uniform (one LDS word after a barrier)
+        singular = true;
+        break;
+      }
+      const float d = sqrtf(dkk), inv = 1.f / d;
+      for (int i = k + 1 + tid; i < n; i += RBF_CH_THREADS) {
+        const float l = S[tri(i, k)] * inv;
+        S[tri(i, k)] = l;
+        col[i] = l;
+      }
+      __syncthreads();
+      if (tid == 0) S[tri(k, k)] = d;
+      for (int i = k + 1 + wave; i < n; i += RBF_CH_THREADS / 64) {
+        const float li = col[i];
+        float* row = S + tri(i, 0);
+        for (int j = k + 1 + lane; j <= i; j += 64) row[j] = fmaf(-li, col[j], row[j]);
+      }
+      __syncthreads();
+    }
+  }
+  if (!singular) {
+    double rd[4], z2[4], mr[4], wr[4];
+    double mz2 = 0.0, mu = 0.0;
+    if (wave == 0) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int i = lane + 64 * s;
+        rd[s] = i < n ? 1.0 / (double)S[tri(i, i)] : 0.0;
+        mr[s] = i < n ? m[i] : 0.0;
+        z2[s] = mr[s];
+      }
+      mu = m[n];
+      chol_solve(S, n, rd, z2, lane);
+      double t = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t = fma(mr[s], z2[s], t);
+      mz2 = wave_sum64(t);
+    }
+    // A⁻¹ r through the bordered Householder system; r: entries lane + 64s (wave 0)
+    auto solve = [&](double (&r)[4]) {
+      double t = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t = fma(lane + 64 * s < N ? u(lane + 64 * s) : 0.0, r[s], t);
+      const double ub = wave_sum64(t);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int i = lane + 64 * s;
+        r[s] = i < N ? fma(-beta * u(i), ub, r[s]) : 0.0;  // c = H r
+      }
+      const double cn = readlane64(pick4(r, n >> 6), n & 63);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (lane + 64 * s >= n) r[s] = 0.0;
+      chol_solve(S, n, rd, r, lane);  // z1
+      t = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t = fma(mr[s], r[s], t);
+      const double yn = (cn + wave_sum64(t)) / (mu + mz2);
+      t = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int i = lane + 64 * s;
+        r[s] = i < n ? fma(z2[s], yn, -r[s]) : (i == n ? yn : 0.0);
+        t = fma(i < N ? u(i) : 0.0, r[s], t);
+      }
+      const double uy = wave_sum64(t);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int i = lane + 64 * s;
+        if (i < N) r[s] = fma(-beta * u(i), uy, r[s]);  // w = H y
+      }
+    };
+    if (wave == 0) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) wr[s] = lane + 64 * s < N ? b[lane + 64 * s] : 0.0;
+      solve(wr);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (lane + 64 * s < N) w[lane + 64 * s] = wr[s];
+    }
+    double dprev = __builtin_inf();
+    for (int it = 0; it < RBF_CH_MAX_REFINE; ++it) {
+      __syncthreads();
+      {  // v = b − A w in fp64, two threads per row
+        const int i = tid >> 1, h = tid & 1;
+        double r = 0.0;
+        if (i < N) {
+          const double xi = xs[i], yi = ys[i];
+          for (int j = h; j < N; j += 2) r = fma(-dist64(xi, yi, xs[j], ys[j]), w[j], r);
+        }
+        r += __shfl_xor(r, 1);
+        if (i < N && h == 0) v[i] = b[i] + r;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        double dv[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) dv[s] = lane + 64 * s < N ? v[lane + 64 * s] : 0.0;
+        solve(dv);
+        double dn = 0.0, wn = 0.0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int i = lane + 64 * s;
+          if (i < N) {
+            wr[s] += dv[s];
+            w[i] = wr[s];
+            dn = fmax(dn, fabs(dv[s]));
+            wn = fmax(wn, fabs(wr[s]));
+          }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          dn = fmax(dn, __shfl_xor(dn, off));
+          wn = fmax(wn, __shfl_xor(wn, off));
+        }
+        if (lane == 0)
+          s_more = dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
+        dprev = dn;
+      }
+      __syncthreads();
+      if (!s_more) break;  // uniform
+    }
+  }
+  if (singular && tid == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
+  __syncthreads();
+  for (int j = tid; j < N; j += RBF_CH_THREADS) wT[(int64_t)j * P + p] = singular ? __builtin_nan("") : w[j];
+}
+
+size_t rbf_chol_lds(int N) {
+  const int n = N - 1;
+  return 7 * (size_t)N * sizeof(double) + (size_t)((N + 3) & ~3) * sizeof(float) +
+         (size_t)n * (n + 1) / 2 * sizeof(float);
+}
+
 // Wave-wide max of a u32 key: DPP within each row of 16 lanes, then the four row maxima
 // through readlane (scalar).  No LDS round trips on the pivot search's critical path.
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
@@ -488,7 +765,12 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
   else if (N <= 80) RBF_GJ(80);
   else if (N <= 96) RBF_GJ(96);
   else if (N <= RBF_GJ_MAX_N) RBF_GJ(112);
-  else {
+  else if (N > RBF_MAX_N) {
+    const size_t lds = rbf_chol_lds(N);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rbf_solve_chol<T>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((rbf_solve_chol<T>), g, dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status);
+  } else {
     const size_t lds = 5 * (size_t)N * sizeof(double) + 2 * (size_t)N * sizeof(int) + (size_t)N * ((N + 2) & ~1) * sizeof(float);
     if (lds > 65536)  // opt in to more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rbf_solve_lds<T>),
@@ -521,7 +803,7 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
                                 rti_stream_t stream) {
   if (!lu || !lv || !I || !luv || !out || !status) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: null pointer");
   if (N <= 0 || P <= 0 || E <= 0) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: N, P, E must be positive");
-  if (N > RBF_MAX_N) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: N=%d > %d lights", N, RBF_MAX_N);
+  if (N > RBF_CH_MAX_N) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: N=%d > %d lights", N, RBF_CH_MAX_N);
   if (P > 0x7fffffff) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: P too large for one launch");
   if (in_dtype != RTI_F32 && in_dtype != RTI_U8 && in_dtype != RTI_I32)
     return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: input dtype %d", in_dtype);

@@ -46,6 +46,7 @@ RTI_KERNEL_STAGE = 0x800
 RTI_KERNEL_CHUNKS_SHIFT = 12  # VALU chunks per lane in bits 12-15 (0 = AUTO)
 RTI_KERNEL_TILE_PLANES_SHIFT = 16  # TILE kernel: light planes per wave and step in bits 16-19 (0 = 2)
 RTI_KERNEL_TILE_DEPTH_SHIFT = 20  # TILE kernel: tiles in the LDS ring in bits 20-23 (0 = 2)
+RTI_KERNEL_TILE_WAVES_SHIFT = 24  # TILE kernel: waves per workgroup in bits 24-27 (0 = 4; 8 = wide form)
 
 
 class RTILibraryMissing(ImportError):

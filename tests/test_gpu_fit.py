@@ -243,3 +243,34 @@ def test_wide_lane_chunks(cuda, chunks, basis, n, in_dtype):
             for c in range(2):
                 err, ok = coef_close(got[c], ref[c])
                 assert ok, (P, layout, c, err)
+
+
+@pytest.mark.parametrize("rc", [4, 8])
+@pytest.mark.parametrize("depth", [2, 3])
+@pytest.mark.parametrize("basis,n", [("hsh", 29), ("hsh", 200), ("hsh9", 10), ("ptm", 37), ("hsh", 16), ("hsh", 24)])
+def test_lds_tile_wide_workgroup(cuda, rc, depth, basis, n):
+    """The 8-wave tile kernel (RTI_KERNEL_TILE_WAVES(8)): one plane per wave and step, plane loads
+    1 (depth 2) or 2 (depth 3) steps ahead; light counts giving 1, 2, 3 (odd) and 25 steps and a
+    partial last step, pixel counts around tile multiples, two channels, both layouts."""
+    k = rti.basis_terms(basis)
+    lu, lv = o.synth_dirs(n, 19)
+    pinv64 = np.linalg.pinv(o.design("hsh" if basis != "ptm" else "ptm", lu, lv)[:, :k])
+    pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=cuda)
+    R = 256 * rc
+    L = rti._lib
+    flags = 0x100 | (rc << L.RTI_KERNEL_CHUNKS_SHIFT) | (depth << L.RTI_KERNEL_TILE_DEPTH_SHIFT) | \
+        (8 << L.RTI_KERNEL_TILE_WAVES_SHIFT)
+    for P in (4, R - 4, R, 3 * R + 260):
+        rng = np.random.default_rng(P + n + rc)
+        I = rng.integers(0, 256, size=(2, n, P)).astype(np.float32)
+        ref = np.einsum("kn,cnp->cpk", pinv64, I.astype(np.float64))
+        for layout in ("pixel", "planar"):
+            coef = torch.full((2, P, k) if layout == "pixel" else (2, k, P), float("nan"), device=cuda)
+            rti.fit_shared_into(pv, torch.as_tensor(I, device=cuda), coef, k=k, layout=layout, kernel="tile",
+                                flags=flags)
+            got = coef.cpu().numpy()
+            if layout == "planar":
+                got = np.moveaxis(got, 1, 2)
+            for c in range(2):
+                err, ok = coef_close(got[c], ref[c])
+                assert ok, (P, layout, c, err)

@@ -165,8 +165,11 @@ def test_compat_default_interpolation_perpixel(cuda):
         compat.interpolate_intensities((d["singular_lx"], d["singular_ly"], d["I"][:1, :1]))
 
 
-@pytest.mark.parametrize("n", [6, 37, 64, 65, 100, 128])
+@pytest.mark.parametrize("n", [6, 37, 64, 65, 100, 112, 113, 128, 129, 160, 200, 255, 256])
 def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
+    """Every solver of rti_rbf_perpixel: register Gauss-Jordan (N <= 112), fp32 LU in LDS (<= 128),
+    Householder-projected Cholesky (<= 256; SURVEY §6 timed the reference at N = 200), each with the
+    reference's per-pixel geometry, against SciPy's fp64 solve restated in the oracle."""
     ys, xs = np.mgrid[0:3, 0:5]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
@@ -177,3 +180,21 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     ref = np.stack([o.rbf_linear(lu[p], lv[p], inten[p], qu, qv) for p in range(15)])
     err, ok = relight_close(out, ref, rtol=1e-8)
     assert ok, err
+
+
+@pytest.mark.parametrize("n", [129, 200, 256])
+def test_rbf_perpixel_large_n_repeated_node_raises(cuda, n):
+    """A repeated light direction makes A exactly singular: SciPy raises LinAlgError; so does the
+    N > 128 solver; N > 256 is refused (RTI_ERR_UNSUPPORTED)."""
+    ys, xs = np.mgrid[0:2, 0:2]
+    rng = np.random.default_rng(n)
+    cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
+    lu, lv = o.light_dirs_for_pixels(cams, xs.ravel(), ys.ravel())
+    lu[2, 7], lv[2, 7] = lu[2, 3], lv[2, 3]
+    inten = rng.integers(0, 256, (4, n)).astype(np.int32)
+    qu, qv = rng.uniform(-1, 1, 50), rng.uniform(-1, 1, 50)
+    with pytest.raises(np.linalg.LinAlgError):
+        rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv)
+    with pytest.raises(NotImplementedError):
+        rti.interpolate_rbf_perpixel(torch.zeros((1, 257), dtype=torch.int32, device=cuda),
+                                     np.zeros((1, 257), np.float32), np.zeros((1, 257), np.float32), qu, qv)

@@ -57,6 +57,8 @@ def main():
                 fl |= int(o[1:]) << 16
             if o[:1] == "d" and o[1:].isdigit():  # d<n>: TILE kernel LDS ring depth
                 fl |= int(o[1:]) << 20
+            if o[:1] == "w" and o[1:].isdigit():  # w<n>: TILE kernel waves per workgroup
+                fl |= int(o[1:]) << 24
         variants.append((v, parts[0], parts[1], fl))
     probe = None
     plib = os.path.join(ROOT, "tools", "probe", "libhbm_probe.so")
