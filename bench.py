@@ -946,9 +946,9 @@ def main():
     for i in range(args.steps):
         wl.step(i)
     torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0  # this rank's K steps; the max over ranks is taken below
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
 
     # kernel duration for the roofline: HIP events around each launch on the launch
     # stream, 10 warm-ups then the median of 50, in a separate pass so the events add no gaps above

@@ -51,11 +51,50 @@ __device__ __forceinline__ float dot_k(const float (&c)[K], const float* b) {
   return acc;
 }
 
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Pixel-major coefficient rows through LDS.  A lane's own 4 pixels are K·sizeof(TC)·4 contiguous
+// bytes, so per-lane loads stride that far across the wave (96 B for PTM-6 fp32) and every
+// 128-B line is requested by several load instructions.  Instead the wave reads its 256 pixels'
+// rows as PIECES coalesced 1-KiB loads (lane l, piece j: bytes 16·(64·j + l) of the chunk),
+// parks them in its LDS slab and reads back its own 4 pixels' rows (cold c5: DESIGN.md §4.4).
+template <int K, typename TC>
+constexpr bool coef_staged() {
+  return (K * sizeof(TC)) % 4 == 0 && 4 * 256 * K * sizeof(TC) <= 48 * 1024;
+}
+
+template <int K, typename TC>
+__device__ __forceinline__ void load_coef_staged(const TC* __restrict__ coef, int64_t wave_px, int lane,
+                                                 floatx4* __restrict__ slab, TC (&c)[4][K]) {
+  constexpr int PIECES = K * (int)sizeof(TC) / 4;  // 16-B pieces per lane (6 for PTM-6 fp32)
+  const floatx4* g = reinterpret_cast<const floatx4*>(coef + wave_px * K);
+  floatx4 t[PIECES];
+#pragma unroll
+  for (int j = 0; j < PIECES; ++j) t[j] = __builtin_nontemporal_load(g + j * 64 + lane);
+#pragma unroll
+  for (int j = 0; j < PIECES; ++j) slab[j * 64 + lane] = t[j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  union {
+    floatx4 v[PIECES];
+    TC c[4][K];
+  } u;
+#pragma unroll
+  for (int j = 0; j < PIECES; ++j) u.v[j] = slab[lane * PIECES + j];
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+#pragma unroll
+    for (int k = 0; k < K; ++k) c[v][k] = u.c[v][k];
+}
+
 // Eval-major: block = 256 lanes × VEC pixels, up to ECH evals (blockIdx.y).
 template <int K, int VEC, typename TC, typename TO, int CL>
 __global__ void __launch_bounds__(256)
 relight_eval_major(const TC* __restrict__ coef, int basis, int64_t P, const double* __restrict__ luv, int E,
                    TO* __restrict__ out) {
+  constexpr bool STAGED = VEC == 4 && CL == RTI_COEF_PIXEL_MAJOR && coef_staged<K, TC>();
+  __shared__ floatx4 slab[STAGED ? 4 * 64 * K * sizeof(TC) / 4 : 1];  // 4 waves × 256 px rows
   __shared__ TC btab[ECH * K];
   const int e0 = blockIdx.y * ECH;
   const int ne = min(ECH, E - e0);
@@ -70,11 +109,20 @@ relight_eval_major(const TC* __restrict__ coef, int basis, int64_t P, const doub
   if (p0 >= P) return;
 
   TC c[VEC][K];
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_px = p0 - 4 * lane;
+  if constexpr (STAGED) {
+    if (wave_px + 256 <= P) {  // wave-uniform: the whole 256-pixel chunk is in the image
+      load_coef_staged<K, TC>(coef, wave_px, lane, slab + (threadIdx.x >> 6) * (64 * K * (int)sizeof(TC) / 4), c);
+      goto evaluate;
+    }
+  }
 #pragma unroll
   for (int v = 0; v < VEC; ++v)
 #pragma unroll
     for (int k = 0; k < K; ++k)
       c[v][k] = (CL == RTI_COEF_PLANAR) ? coef[(int64_t)k * P + p0 + v] : coef[(p0 + v) * K + k];
+evaluate:
 
   for (int e = 0; e < ne; ++e) {
     const TC* b = btab + e * K;
@@ -138,7 +186,7 @@ void launch_t(const RelightArgs& a) {
     return;
   }
   const unsigned ey = (unsigned)((a.E + ECH - 1) / ECH);
-  const bool vec = a.P % 4 == 0 && aligned_to(a.out, 4 * sizeof(TO)) && aligned_to(a.coef, sizeof(TC));
+  const bool vec = a.P % 4 == 0 && aligned_to(a.out, 4 * sizeof(TO)) && aligned_to(a.coef, 16);
   if (vec)
     hipLaunchKernelGGL((relight_eval_major<K, 4, TC, TO, CL>), dim3(grid_1d(a.P / 4, 256), ey), dim3(256), 0, a.s,
                        coef, a.basis, a.P, a.luv, a.E, out);
@@ -223,10 +271,25 @@ template <int K, typename TC, int CL>
 __global__ void __launch_bounds__(256)
 relight_frame_k(const void* __restrict__ src, int basis, int64_t P, double lu, double lv,
                 const uint8_t* __restrict__ hsv, uint8_t* __restrict__ bgr) {
+  constexpr bool STAGED = K > 0 && CL == RTI_COEF_PIXEL_MAJOR && coef_staged<K, TC>();
+  __shared__ floatx4 slab[STAGED ? 4 * 64 * K * sizeof(TC) / 4 : 1];  // 4 waves × 256 px rows
   const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (p0 >= P) return;
   const int np = P - p0 < 4 ? (int)(P - p0) : 4;
   uint8_t Vv[4];
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_px = p0 - 4 * lane;
+  if constexpr (STAGED) {
+    if (wave_px + 256 <= P && aligned_to(src, 16)) {  // wave-uniform
+      TC b[K], c[4][K];
+      basis_eval<TC>(basis, (TC)lu, (TC)lv, b);
+      load_coef_staged<K, TC>(static_cast<const TC*>(src), wave_px, lane,
+                              slab + (threadIdx.x >> 6) * (64 * K * (int)sizeof(TC) / 4), c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Vv[j] = cvt_out<uint8_t>(dot_k<K>(c[j], b));
+      goto convert;
+    }
+  }
   if constexpr (K == 0) {
     const int32_t* t = static_cast<const int32_t*>(src);
 #pragma unroll
@@ -247,6 +310,7 @@ relight_frame_k(const void* __restrict__ src, int basis, int64_t P, double lu, d
       Vv[j] = cvt_out<uint8_t>(dot_k<K>(c, b));
     }
   }
+convert:
   uint8_t in[12], o[12];
   const uint8_t* hp = hsv + p0 * 3;
   uint8_t* op = bgr + p0 * 3;
