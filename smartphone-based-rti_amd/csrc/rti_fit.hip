@@ -434,6 +434,8 @@ fit_shared_tile(const float* __restrict__ pinv, int k, int N, const T* __restric
 // register-staged kernel above has one, 64 KiB per CU).  Each wave computes R/W pixels of every
 // step (acc = 4·R/(64·W) floatx4: 64 VGPRs at R = 2048, W = 8), so the MFMA accumulators shrink
 // as the waves grow and the registers go to loads in flight instead.
+// AHEAD = 0: ONE LDS tile (half the LDS, so twice the tile width fits: 16 KiB runs per wave and
+// plane at RC = 16), the next step's loads in registers during the compute, two barriers per step.
 template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT>
 __global__ void __launch_bounds__(64 * W)
 fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P,
@@ -443,7 +445,7 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   const int T_ = (N + S - 1) / S;  // steps
   float* __restrict__ lds_pinv = lds_dyn;             // [T_·S][16]
-  float* __restrict__ tile = lds_dyn + T_ * S * 16;  // [2][S][R]
+  float* __restrict__ tile = lds_dyn + T_ * S * 16;  // [2][S][R] ([1][S][R] at AHEAD = 0)
   for (int idx = threadIdx.x; idx < T_ * S * 16; idx += 64 * W) {
     const int n = idx >> 4, i = idx & 15;
     lds_pinv[idx] = (i < k && n < N) ? pinv[i * N + n] : 0.f;
@@ -495,7 +497,18 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
   }
   park(0, sa);
   __syncthreads();
-  if constexpr (AHEAD == 1) {
+  if constexpr (AHEAD == 0) {
+    for (int t = 0; t < T_; ++t) {
+      const bool more = t + 1 < T_;  // workgroup-uniform
+      if (more) load(t + 1, sa);
+      compute(0, t);
+      __syncthreads();
+      if (more) {
+        park(0, sa);
+        __syncthreads();
+      }
+    }
+  } else if constexpr (AHEAD == 1) {
     for (int t = 0; t < T_; ++t) {
       const bool more = t + 1 < T_;  // workgroup-uniform
       if (more) load(t + 1, sa);
@@ -827,7 +840,7 @@ template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT>
 int launch_tile_w_t(const FitArgs& a) {
   constexpr int R = 256 * RC, S = W;
   const int T_ = (a.N + S - 1) / S;
-  const size_t lds = ((size_t)T_ * S * 16 + (size_t)2 * S * R) * sizeof(float);
+  const size_t lds = ((size_t)T_ * S * 16 + (size_t)(AHEAD == 0 ? 1 : 2) * S * R) * sizeof(float);
   if (lds > 160 * 1024)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
   auto kern = fit_shared_tile_w<RC, W, AHEAD, T, LAYOUT, NT>;
@@ -850,7 +863,9 @@ int launch_tile_w_l(const FitArgs& a) {
               : launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PIXEL_MAJOR, false>(a);
 }
 
+// depth 1: one LDS tile (AHEAD 0, rc up to 16), 2: double tile, loads 1 step ahead, 3: loads 2 ahead
 int launch_tile_w(const FitArgs& a, int rc, int depth) {
+  if (depth == 1) return rc >= 12 ? launch_tile_w_l<16, 0>(a) : launch_tile_w_l<8, 0>(a);  // CHUNKS(15) = 16
   if (rc >= 8) return depth >= 3 ? launch_tile_w_l<8, 2>(a) : launch_tile_w_l<8, 1>(a);
   return depth >= 3 ? launch_tile_w_l<4, 2>(a) : launch_tile_w_l<4, 1>(a);
 }
@@ -1008,15 +1023,22 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
   const bool auto_tile = sel == RTI_KERNEL_AUTO && k == 16 && in_dtype == RTI_F32 && P * C >= (int64_t)1024 * 2048;
   if (sel == RTI_KERNEL_TILE || (auto_tile && mfma_ok)) {
     if (mfma_ok) {
-      // default tile: 2048 pixels x 8 planes per step, register-staged (1024 pixels above N = 512,
-      // where the 128 KiB double tile and the [N][16] pseudo-inverse no longer fit 160 KiB of LDS)
+      // explicit tile bits: the 4-wave kernels (2048 pixels x 8 planes per step, register-staged, or
+      // the DMA ring) or the 8-wave kernels; 1024-pixel tiles above N = 512
       const int rc = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, sp = (kernel >> RTI_KERNEL_TILE_PLANES_SHIFT) & 0xF;
       const int depth = (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF;
       const int waves = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF;
+      // AUTO (no tile bits set) for fp32 at N <= 512: the 8-wave kernel on ONE 4096-pixel LDS tile
+      // (16 KiB per wave and plane; c4 3.74 vs 3.93 ms for the 2048-pixel double-buffered tile,
+      // profiles/r02_c4_tile_rc16_sweep.log); above N = 512 its [N][16] pinv no longer fits.
+      const bool tile_auto = (kernel & ~0xff & ~RTI_KERNEL_NONTEMPORAL) == 0 && N <= 512;
       const int rc0 = rc ? rc : (N <= 512 ? 8 : 4);
       int st;
       switch (in_dtype) {
-        case RTI_F32: st = launch_tile<float>(a, rc0, sp ? sp : 2, depth ? depth : 2, waves); break;
+        case RTI_F32:
+          st = tile_auto ? launch_tile<float>(a, 15, 1, 1, 8)
+                         : launch_tile<float>(a, rc0, sp ? sp : 2, depth ? depth : 2, waves);
+          break;
         case RTI_I32: st = launch_tile<int32_t>(a, 4, 1, 2, 4); break;
         default: st = launch_tile<uint8_t>(a, 4, 1, 2, 4); break;
       }

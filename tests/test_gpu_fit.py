@@ -245,18 +245,19 @@ def test_wide_lane_chunks(cuda, chunks, basis, n, in_dtype):
                 assert ok, (P, layout, c, err)
 
 
-@pytest.mark.parametrize("rc", [4, 8])
-@pytest.mark.parametrize("depth", [2, 3])
+@pytest.mark.parametrize("rc,depth", [(4, 2), (4, 3), (8, 2), (8, 3), (8, 1), (15, 1)])
 @pytest.mark.parametrize("basis,n", [("hsh", 29), ("hsh", 200), ("hsh9", 10), ("ptm", 37), ("hsh", 16), ("hsh", 24)])
 def test_lds_tile_wide_workgroup(cuda, rc, depth, basis, n):
     """The 8-wave tile kernel (RTI_KERNEL_TILE_WAVES(8)): one plane per wave and step, plane loads
-    1 (depth 2) or 2 (depth 3) steps ahead; light counts giving 1, 2, 3 (odd) and 25 steps and a
-    partial last step, pixel counts around tile multiples, two channels, both layouts."""
+    1 (depth 2) or 2 (depth 3) steps ahead, or one LDS tile (depth 1, rc 8 or 15 -> 16 chunks);
+    light counts giving 1, 2, 3 (odd) and 25 steps and a partial last step, pixel counts around tile
+    multiples, two channels, both layouts."""
+    rc_eff = 16 if rc >= 12 else rc
     k = rti.basis_terms(basis)
     lu, lv = o.synth_dirs(n, 19)
     pinv64 = np.linalg.pinv(o.design("hsh" if basis != "ptm" else "ptm", lu, lv)[:, :k])
     pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=cuda)
-    R = 256 * rc
+    R = 256 * rc_eff
     L = rti._lib
     flags = 0x100 | (rc << L.RTI_KERNEL_CHUNKS_SHIFT) | (depth << L.RTI_KERNEL_TILE_DEPTH_SHIFT) | \
         (8 << L.RTI_KERNEL_TILE_WAVES_SHIFT)

@@ -24,10 +24,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--variants", default="0,1,2,3,4")
-    ap.add_argument("--gy", type=int, default=1)
+    ap.add_argument("--gy", type=int, default=1, help="variants 0-4: row-block split; 5-7: pixel segments")
+    ap.add_argument("--segs", type=int, default=32, help="pixel segments of the row-sweep variants 5-7")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    w = bench.OperatorWorkload(types.SimpleNamespace(op_precision="split16"), bench.CONFIGS["c7"], 0, dev)
+    cfg = bench.CONFIGS["c7"]
+    ns = types.SimpleNamespace(op_precision="split16", weak=False, config="c7")
+    w = bench.OperatorWorkload(ns, cfg, bench.Ctx(ns, cfg[1], 0, 1, dev))
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "probe", "libstore_probe.so"))
     lib.probe_store_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_void_p]
@@ -39,7 +42,7 @@ def main():
         if v is None:
             w.step(0)
         else:
-            assert lib.probe_store_rows(ctypes.c_void_p(sink.data_ptr()), w.E, w.P, v, args.gy,
+            assert lib.probe_store_rows(ctypes.c_void_p(sink.data_ptr()), w.E, w.P, v, args.segs if v >= 5 else args.gy,
                                         ctypes.c_void_p(stream.cuda_stream)) == 0
 
     for name, v in runs:
