@@ -854,13 +854,13 @@ int launch_tile_w_t(const FitArgs& a) {
 }
 
 // wide-workgroup tile (fp32): rc 4 or 8, 8 waves, loads 1 or 2 steps ahead
-template <int RC, int AHEAD>
+template <int RC, int AHEAD, int W = 8>
 int launch_tile_w_l(const FitArgs& a) {
   if (a.layout == RTI_COEF_PLANAR)
-    return a.nt ? launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PLANAR, true>(a)
-                : launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PLANAR, false>(a);
-  return a.nt ? launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PIXEL_MAJOR, true>(a)
-              : launch_tile_w_t<RC, 8, AHEAD, float, RTI_COEF_PIXEL_MAJOR, false>(a);
+    return a.nt ? launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, true>(a)
+                : launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, false>(a);
+  return a.nt ? launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PIXEL_MAJOR, true>(a)
+              : launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PIXEL_MAJOR, false>(a);
 }
 
 // depth 1: one LDS tile (AHEAD 0, rc up to 16), 2: double tile, loads 1 step ahead, 3: loads 2 ahead
@@ -868,6 +868,14 @@ int launch_tile_w(const FitArgs& a, int rc, int depth) {
   if (depth == 1) return rc >= 12 ? launch_tile_w_l<16, 0>(a) : launch_tile_w_l<8, 0>(a);  // CHUNKS(15) = 16
   if (rc >= 8) return depth >= 3 ? launch_tile_w_l<8, 2>(a) : launch_tile_w_l<8, 1>(a);
   return depth >= 3 ? launch_tile_w_l<4, 2>(a) : launch_tile_w_l<4, 1>(a);
+}
+
+// 4-wave form of the same kernel at one wave per SIMD: a 4096-pixel tile (16 KiB per wave and
+// plane), 4 planes per step, the tile double-buffered (2 x 64 KiB) so one barrier per step, and
+// the 256 accumulator registers per lane (16 pixel groups x 4 floatx4) in the AGPR half of the
+// unified 512-register file, which leaves the VGPRs to loads 1 (depth 2) or 2 (depth 3) steps ahead.
+int launch_tile_w4(const FitArgs& a, int depth) {
+  return depth >= 3 ? launch_tile_w_l<16, 2, 4>(a) : launch_tile_w_l<16, 1, 4>(a);
 }
 
 template <int RC, int SP, int NB, int LAYOUT, bool NT>
@@ -909,6 +917,7 @@ template <typename T>
 int launch_tile(const FitArgs& a, int rc, int sp, int depth, int waves) {
   if constexpr (std::is_same<T, float>::value) {
     if (waves == 8) return launch_tile_w(a, rc, depth);
+    if (waves == 4 && rc >= 12) return launch_tile_w4(a, depth);
     if (depth >= 4) return launch_tile_dma<4>(a, rc, sp);
     if (depth == 3) return launch_tile_dma<3>(a, rc, sp);
   }

@@ -161,10 +161,17 @@ int launch_res(const ResArgs& a) {
 // Chunks per lane, measured at 4K x 100 (profiles/r01_residual_c3_nc_sweep.log): PTM-6
 // NC = 1 / 2 / 4 / 8 -> 0.522 / 0.520 / 0.505 / 0.578 ms (8 chunks = 256 VGPRs, 1 wave/SIMD,
 // cannot hide the coefficient loads).  HSH-9/16 keep one chunk (wide lanes not measured).
+// The wide form needs enough waves to cover the chip (1024 SIMDs, 2 waves each at 4 chunks);
+// the cutoff is the fit's heuristic (rti_fit.hip AUTO: >= 2000 waves), not a residual sweep.
+constexpr int64_t kResWideMinWaves = 2000;
+
 template <int K, typename T>
 int launch_res_v(const ResArgs& a, bool vec4) {
   if (!vec4) return launch_res<K, 1, 1, T>(a);
-  if (K == 6 && a.P * a.C / (64 * 4 * 4) >= 2000) return launch_res<K, 4, (K == 6 ? 4 : 1), T>(a);
+  if constexpr (K == 6) {
+    constexpr int NC = 4;
+    if (a.P * a.C / (64 * 4 * NC) >= kResWideMinWaves) return launch_res<K, 4, NC, T>(a);
+  }
   return launch_res<K, 4, 1, T>(a);
 }
 

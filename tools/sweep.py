@@ -105,9 +105,18 @@ def main():
         else:
             rti.fit_shared_into(pv, I, coefs[layout], k=k, layout=layout, kernel=kern, flags=fl)
 
+    agree = {}  # every library variant's coefficients against the first library variant's
+    ref = None
     for name, kern, layout, fl in variants:  # warm-up
         for _ in range(3):
             launch(kern, layout, fl)
+        if kern in ("valu", "mfma", "tile", "auto"):
+            got = coefs[layout] if layout == "pixel" else coefs[layout].transpose(1, 2)
+            got = got.double()
+            if ref is None:
+                ref = got.clone()
+            scale = ref.abs().amax(-1, keepdim=True).clamp_min(1e-30)
+            agree[name] = float(((got - ref).abs() / scale).max())
     torch.cuda.synchronize()
     for _ in range(args.rounds):
         for name, kern, layout, fl in variants:
@@ -124,8 +133,11 @@ def main():
         byts = 4.0 * P * N if name.startswith("probe_read") else (4.0 * P * k if name.startswith("probe_write") else alg)
         res[name] = {"median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
                      "GBps_median": byts / (np.median(ms) * 1e-3) / 1e9}
+        if name in agree:
+            res[name]["max_rel_vs_first"] = agree[name]
         print(f"{name:24s} median {np.median(ms):.4f} ms  min {ms.min():.4f} ms  "
-              f"{res[name]['GBps_median']:.0f} GB/s ({res[name]['GBps_median'] / 80:.1f}% of 8 TB/s)", flush=True)
+              f"{res[name]['GBps_median']:.0f} GB/s ({res[name]['GBps_median'] / 80:.1f}% of 8 TB/s)"
+              + (f"  rel {agree[name]:.1e}" if name in agree else ""), flush=True)
     print(json.dumps({"config": args.config, "results": res}))
 
 
