@@ -336,7 +336,9 @@ class FitResidualWorkload(FitWorkload):
         self.dtype = "f32 in / f64 accumulate / f32 out"
 
     def traffic(self):
-        return None
+        if self.ctx.world != 1 or self.ctx.weak:
+            return None
+        return load_traffic(self.args.config)
 
     def parity(self):
         o = oracle()

@@ -62,19 +62,25 @@ def main():
         variants.append((v, parts[0], parts[1], fl))
     probe = None
     plib = os.path.join(ROOT, "tools", "probe", "libhbm_probe.so")
-    if os.path.exists(plib) and C == 1 and not args.no_probe:
+    tlib = os.path.join(ROOT, "tools", "probe", "libtile_probe.so")
+    if os.path.exists(tlib) and k == 16 and not args.no_probe:
+        tprobe = ctypes.CDLL(tlib)
+        tprobe.probe_tile_nostore.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        variants.append(("probe_tile_nostore", "ptile", "0", 0))
+    if os.path.exists(plib) and not args.no_probe:
         probe = ctypes.CDLL(plib)
         probe.probe_read.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_void_p]
         probe.probe_fit6.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         sink = torch.zeros(1, device=dev)
-        for pvnt in (0, 1, 2, 3, 4):
+        for pvnt in (0, 1, 2, 3, 4):  # C channels = C*N light planes of one [C*N][P] stack
             variants.append((f"probe_read_v{pvnt}", "probe", str(pvnt), 0))
         probe.probe_store.argtypes = probe.probe_fit6.argtypes
         probe.probe_write.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
         variants.append(("probe_write_coef_bytes", "pwrite", "0", 0))
-        if k == 6:
+        if k == 6 and C == 1:
             for pvnt, nm in ((1, "nostore"),):
                 variants.append((f"probe_fit6_{nm}", "pfit", str(pvnt), 0))
             for pvnt, nm in ((0, "plain"), (4, "win64K")):
@@ -87,10 +93,14 @@ def main():
 
     def launch(kern, layout, fl):
         if kern == "probe":
-            probe.probe_read(ctypes.c_void_p(I.data_ptr()), N, P, ctypes.c_void_p(sink.data_ptr()), int(layout),
+            probe.probe_read(ctypes.c_void_p(I.data_ptr()), N * C, P, ctypes.c_void_p(sink.data_ptr()), int(layout),
                              ctypes.c_void_p(stream.cuda_stream))
+        elif kern == "ptile":
+            tprobe.probe_tile_nostore(ctypes.c_void_p(pv.data_ptr()), k, N, ctypes.c_void_p(I.data_ptr()), P, C,
+                                      ctypes.c_void_p(coefs["pixel"].data_ptr()), ctypes.c_void_p(stream.cuda_stream))
         elif kern == "pwrite":
-            probe.probe_write(ctypes.c_void_p(coefs["pixel"].data_ptr()), 4 * P * k, ctypes.c_void_p(stream.cuda_stream))
+            probe.probe_write(ctypes.c_void_p(coefs["pixel"].data_ptr()), 4 * P * k * C,
+                              ctypes.c_void_p(stream.cuda_stream))
         elif kern == "ppersist":
             probe.probe_persist(ctypes.c_void_p(pv.data_ptr()), ctypes.c_void_p(I.data_ptr()), N, P,
                                 ctypes.c_void_p(coefs["pixel"].data_ptr()), int(layout),
@@ -130,7 +140,8 @@ def main():
     res = {}
     for name, *rest in variants:
         ms = np.array([a.elapsed_time(b) for a, b in times[name]])
-        byts = 4.0 * P * N if name.startswith("probe_read") else (4.0 * P * k if name.startswith("probe_write") else alg)
+        byts = 4.0 * P * N * C if name.startswith(("probe_read", "probe_tile_nostore")) else \
+            (4.0 * P * k * C if name.startswith("probe_write") else alg)
         res[name] = {"median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
                      "GBps_median": byts / (np.median(ms) * 1e-3) / 1e9}
         if name in agree:
