@@ -7,13 +7,14 @@
 // (LAPACK gesv: LU with partial pivoting) and evaluates f(q) = Σ_j w_j ‖q − x_j‖
 // on the 100×100 grid.  Every pixel has its own light list (compute_intensities,
 // analysis.py:225-231), so there is no shared operator: one workgroup owns one
-// pixel and solves its N×N system — fp64 Gauss-Jordan in registers up to N = 112, fp32 LU in LDS
-// + fp64 iterative refinement up to 128, Householder-projected fp32 Cholesky (packed triangle in
-// LDS) + fp64 refinement up to 256 (the systems reach cond ≈ 1e4–1e5 at N = 100–200) — and a
-// second kernel streams the E evaluations in fp64.
+// pixel and solves its N×N system — fp64 Gauss-Jordan in registers up to N = 80, above that
+// (to N = 256; the systems reach cond ≈ 1e4–1e5 at N = 100–200) an fp32 Gauss-Jordan inverse of
+// the Householder-projected system held in registers as 8×8 blocks, plus fp64 iterative
+// refinement — and a second kernel streams the E evaluations in fp64.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 
 #include "rti_convert.h"
@@ -22,8 +23,7 @@
 namespace rti {
 namespace {
 
-constexpr int RBF_MAX_N = 128;      // rbf_solve_lds (fp32 LU in LDS) up to here; Householder-Cholesky above
-constexpr int RBF_MAX_REFINE = 10;  // refinement sweeps of the fp32-LU fallback
+constexpr int RBF_MAX_N = 256;  // largest N of rbf_solve_gji (an 8·32-row block grid)
 
 template <typename T>
 __device__ __forceinline__ double ldd(const T* p) {
@@ -59,515 +59,293 @@ __device__ __forceinline__ double readlane64(double x, int l) {
   return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 
-// Per-lane view of the fp32 factors for wave 0's triangular solves.  The factorization
-// never moves rows: physical row i became the pivot of step so[i]; A[i][k] holds the
-// multiplier l_ik for k < so[i] and the U entry u_{so[i],k} for k ≥ so[i].  Lane l owns
-// physical rows l and l + 64 (N ≤ 128); the pivot list and the reciprocal diagonal are
-// lane-distributed by step and broadcast with readlane.
-struct LuLane {
-  int r0, r1;    // physical rows (clamped to N − 1 for the address when absent)
-  int s0, s1;    // their pivot steps (N when the row does not exist)
-  int pk0, pk1;  // piv[lane], piv[lane + 64]
-  double rd0, rd1;  // 1 / u_kk for k = lane, lane + 64
-};
+// ---- Register-blocked Gauss-Jordan inverse + fp64 refinement (N ≤ 256) ---------------------------
+// A of distinct nodes is symmetric and strictly conditionally negative definite (negative definite
+// on 1^⊥).  With the Householder reflector H that maps e = 1/√N onto the last unit vector,
+// HAH = [M m; mᵀ μ] has S = −M symmetric positive definite of order n = N − 1, and A w = b is solved
+// by block elimination of the bordered system:
+//   c = H b,  z1 = S⁻¹ c₁,  z2 = S⁻¹ m,  y_n = (c_n + mᵀz1)/(μ + mᵀz2),  y₁ = −z1 + z2·y_n,  w = H y.
+// S is INVERTED in fp32 by in-place Gauss-Jordan without pivoting (stable on SPD matrices: every
+// pivot is a positive Schur complement) and the inverse never leaves the registers: an NB×NB grid of
+// threads (NB = 16 for N ≤ 128, 32 for N ≤ 256) each holds one 8×8 block of S in 64 VGPRs.  Step k:
+// the threads owning row k and column k publish them to LDS (16 floats each, double-buffered, ONE
+// barrier per step), every thread reads the 8 + 8 entries that meet its block and does a rank-1
+// update of its 64 entries:
+//     a_ij ← a_ij − a_ik·a_kj/a_kk,  a_ik ← −a_ik/a_kk,  a_kj ← a_kj/a_kk,  a_kk ← 1/a_kk
+// (one FMA per entry: the pivot row and column are folded into the multipliers, see the step).
+// LDS traffic is 64 B per thread and step, and no step is serial on one wave: the triangular
+// substitutions of a factorization (N dependent steps, repeated every refinement sweep) become
+// matrix-vector products with the explicit inverse, reduced across each block row in registers.
+// The fp32 inverse is the approximate inverse of mixed-precision iterative refinement: residuals
+// b − A·w in fp64 from the node coordinates (correctly rounded sqrt, so A is pdist's), corrections
+// through the bordered system, until the fp64 floor — the weights are SciPy's fp64 LU solution to
+// rounding.  It contracts the error by ≈1e-5 per sweep at cond(A) ≈ 1e4–1e5; at least 3 sweeps run
+// (2 left 3e-10 of max(|f|, 255) against SciPy at N = 200, 3 give 2e-11, the fp64 floor).  Exactly
+// repeated nodes (SciPy: LinAlgError) are detected up front, a non-positive pivot (cond beyond
+// fp32) reports the same status.
+constexpr int RBF_GJI_MAX_REFINE = 16;
 
-// z = U⁻¹ L⁻¹ P v on (v0, v1) = v at physical rows (lane, lane + 64); on return the
-// value held for physical row i is z at node so[i].  Column-oriented, one wave, the
-// chain runs through registers (readlane) and only the factor columns come from LDS.
-__device__ __forceinline__ void lu_solve_regs(const float* A, int lda, int N, const LuLane& q, double& v0,
-                                              double& v1, int lane) {
-  float c0 = A[q.r0 * lda], c1 = A[q.r1 * lda];
-  for (int k = 0; k < N; ++k) {  // forward: rows not yet pivoted at step k lose l_ik · y_k
-    const float n0 = A[q.r0 * lda + min(k + 1, N - 1)], n1 = A[q.r1 * lda + min(k + 1, N - 1)];
-    const int p = __builtin_amdgcn_readlane(k < 64 ? q.pk0 : q.pk1, k & 63);
-    const double y = readlane64(p < 64 ? v0 : v1, p & 63);
-    if (q.s0 > k) v0 = fma(-(double)c0, y, v0);
-    if (q.s1 > k) v1 = fma(-(double)c1, y, v1);
-    c0 = n0, c1 = n1;
-  }
-  c0 = A[q.r0 * lda + N - 1], c1 = A[q.r1 * lda + N - 1];
-  for (int k = N - 1; k >= 0; --k) {  // backward: z_k = y_k / u_kk; earlier pivots lose u_ik · z_k
-    const float n0 = A[q.r0 * lda + max(k - 1, 0)], n1 = A[q.r1 * lda + max(k - 1, 0)];
-    const int p = __builtin_amdgcn_readlane(k < 64 ? q.pk0 : q.pk1, k & 63);
-    const double z = readlane64(p < 64 ? v0 : v1, p & 63) * readlane64(k < 64 ? q.rd0 : q.rd1, k & 63);
-    if (q.s0 == k) v0 = z;
-    if (q.s1 == k) v1 = z;
-    if (q.s0 < k) v0 = fma(-(double)c0, z, v0);
-    if (q.s1 < k) v1 = fma(-(double)c1, z, v1);
-    c0 = n0, c1 = n1;
-  }
+// Lane reductions without address registers: DPP inside each row of 16 lanes (quad_perm 1032,
+// quad_perm 2301, row_half_mirror, row_mirror leave the row's total in all 16 lanes) and
+// ds_swizzle xor 16 across row pairs.  (__shfl_xor keeps a permute-address VGPR per offset alive
+// across the whole kernel, which here pushed the 64-register S⁻¹ block into scratch.)
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double swz_xor16(double v) {  // bit mode: and 0x1F, or 0, xor 0x10
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_ds_swizzle((int)(uint32_t)u, 0x401F);
+  const uint32_t hi = __builtin_amdgcn_ds_swizzle((int)(uint32_t)(u >> 32), 0x401F);
+  return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+template <bool MAX>
+__device__ __forceinline__ double comb(double a, double b) { return MAX ? fmax(a, b) : a + b; }
+template <bool MAX>
+__device__ __forceinline__ double row16_reduce(double v) {
+  v = comb<MAX>(v, dpp64<0xB1>(v));
+  v = comb<MAX>(v, dpp64<0x4E>(v));
+  v = comb<MAX>(v, dpp64<0x141>(v));
+  return comb<MAX>(v, dpp64<0x140>(v));
 }
 
-// Fallback for 112 < N ≤ 128 (register budget of rbf_solve_gj).
-// One workgroup (4 waves) per pixel.  The distance matrix is factored in fp32 in LDS
-// (LU with partial pivoting; 40 KB at N = 100, so several pixels share a CU) and the
-// solution is brought to fp64 accuracy by mixed-precision iterative refinement: the
-// residual b − A·w is formed in fp64 from the node coordinates (A is never stored in
-// fp64) and the correction solved with the fp32 factors.  Each sweep shrinks the error
-// by ≈cond(A)·2⁻²⁴ (≤ 6e-3 up to cond 1e5); sweeps stop when the correction stops
-// shrinking or falls below 1e-16 of the solution.
-//
-// Elimination: rows are never swapped.  Wave w owns physical rows i ≡ w (mod 4) and
-// keeps the not-yet-pivoted ones in a bit mask; lanes own columns.  Step k updates the
-// wave's remaining rows against pivot row p and, in the same pass, lane 0 (column k+1)
-// tracks the largest |a_i,k+1| — the next pivot candidate — so a step costs one barrier.
-template <typename T>
-__global__ void __launch_bounds__(256)
-rbf_solve_lds(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
-              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int lda = (N + 2) & ~1;  // even row pitch (floats) with ≥ 1 zero pad column: 8-byte pairs
-  double* xs = smem;      // [N] node coordinates (fp64 copies of the fp32 light vectors)
-  double* ys = xs + N;    // [N]
-  double* b = ys + N;     // [N] intensities (the right-hand side)
-  double* w = b + N;      // [N] solution, by node
-  double* v = w + N;      // [N] residual, by physical row
-  int* piv = reinterpret_cast<int*>(v + N);  // [N] pivot row of each step
-  int* so = piv + N;                         // [N] pivot step of each row
-  float* A = reinterpret_cast<float*>(so + N);  // [N][lda] fp32 LU factors
-  __shared__ float s_pmax[2][4];
-  __shared__ int s_pidx[2][4];
-  __shared__ int s_more;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: row ownership, masks, branches
-  const int64_t p = blockIdx.x;
-  const int64_t base = p * N;
+template <int NB>
+__device__ __forceinline__ double row_sum(double v) {  // over the NB lanes of one block row (its first lane)
+  v = row16_reduce<false>(v);
+  if constexpr (NB == 32) v += swz_xor16(v);
+  return v;
+}
 
-  for (int j = tid; j < N; j += 256) {
-    xs[j] = (double)lu[base + j];  // SciPy holds float64 copies of the float32 nodes
-    ys[j] = (double)lv[base + j];
-    b[j] = ldd(I + base + j);
-  }
+template <int WAVES, bool MAX>
+__device__ __forceinline__ double block_reduce(double v, double* red) {  // every thread gets the result
+  v = row16_reduce<MAX>(v);
+  v = comb<MAX>(v, swz_xor16(v));
+  v = comb<MAX>(readlane64(v, 0), readlane64(v, 32));
+  __syncthreads();  // the previous reduction's readers are done with red
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int idx = tid; idx < N * lda; idx += 256) {
-    const int i = idx / lda, j = idx - i * lda;
-    A[idx] = j < N ? (float)dist64(xs[i], ys[i], xs[j], ys[j]) : 0.f;
-  }
-  __syncthreads();
-
-  uint32_t mask = 0;  // this wave's rows that are not pivots yet (bit s ↔ row wave + 4s)
-  {
-    const int i = wave + 4 * lane;
-    float best = -1.f;
-    int bi = N;
-    if (lane < 32 && i < N) best = fabsf(A[i * lda]), bi = i;
-    mask = __builtin_amdgcn_readfirstlane((uint32_t)__ballot(lane < 32 && i < N));
+  double r = red[0];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const float ob = __shfl_xor(best, off);
-      const int oi = __shfl_xor(bi, off);
-      if (ob > best || (ob == best && oi < bi)) best = ob, bi = oi;
-    }
-    if (lane == 0) s_pmax[0][wave] = best, s_pidx[0][wave] = bi;
-  }
-
-  bool singular = false;
-  for (int k = 0; k < N; ++k) {
-    __syncthreads();
-    float best = s_pmax[k & 1][0];
-    int pr = s_pidx[k & 1][0];
-#pragma unroll
-    for (int q = 1; q < 4; ++q) {
-      const float ob = s_pmax[k & 1][q];
-      const int oi = s_pidx[k & 1][q];
-      if (ob > best || (ob == best && oi < pr)) best = ob, pr = oi;
-    }
-    pr = __builtin_amdgcn_readfirstlane(pr);  // identical on every lane
-    if (!(best > 0.f)) {  // block-uniform: an exactly zero pivot column
-      singular = true;
-      break;
-    }
-    if (tid == 0) piv[k] = pr, so[pr] = k;
-    if ((pr & 3) == wave) mask &= ~(1u << (pr >> 2));
-    const float inv = 1.f / A[pr * lda + k];
-    // lane l owns the column pair (kb + 2l, kb + 2l + 1), kb = k rounded down to even:
-    // one 8-byte LDS access per row.  Pivot entries at columns ≤ k are zeroed so those
-    // columns pass through unchanged, and column k receives the multiplier l_ik.
-    const int kb = k & ~1, c0 = kb + 2 * lane;
-    const bool kodd = k & 1;
-    float bm = -1.f;
-    int bidx = N;
-    if (c0 < N) {
-      float2 pp = *reinterpret_cast<const float2*>(A + pr * lda + c0);
-      if (c0 <= k) pp.x = 0.f;
-      if (c0 + 1 <= k) pp.y = 0.f;
-      const bool put0 = lane == 0 && !kodd, put1 = lane == 0 && kodd;
-      // rows in batches of RB: all LDS reads of a batch are issued before its first use
-      constexpr int RB = 8;
-      for (uint32_t m = mask; m;) {
-        int ri[RB];
-        float lk[RB];
-        float2 av[RB];
-#pragma unroll
-        for (int t = 0; t < RB; ++t) {
-          ri[t] = m ? wave + 4 * __builtin_ctz(m) : -1;
-          m &= m - 1;
-        }
-#pragma unroll
-        for (int t = 0; t < RB; ++t)
-          if (ri[t] >= 0) {
-            const float* row = A + ri[t] * lda;
-            lk[t] = row[k];
-            av[t] = *reinterpret_cast<const float2*>(row + c0);
-          }
-#pragma unroll
-        for (int t = 0; t < RB; ++t)
-          if (ri[t] >= 0) {
-            const float l = lk[t] * inv;
-            float2 n;
-            n.x = put0 ? l : fmaf(-l, pp.x, av[t].x);
-            n.y = put1 ? l : fmaf(-l, pp.y, av[t].y);
-            *reinterpret_cast<float2*>(A + ri[t] * lda + c0) = n;
-            const float tv = fabsf(kodd ? n.x : n.y);  // column k + 1 on lane (k & 1)
-            if (tv > bm) bm = tv, bidx = ri[t];
-          }
-      }
-    }
-    if (lane == (k & 1)) s_pmax[(k + 1) & 1][wave] = bm, s_pidx[(k + 1) & 1][wave] = bidx;
-  }
-  if (singular && tid == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
-  __syncthreads();
-
-  if (!singular) {
-    LuLane q;
-    double v0 = 0.0, v1 = 0.0;
-    if (wave == 0) {
-      q.r0 = min(lane, N - 1), q.r1 = min(lane + 64, N - 1);
-      q.s0 = lane < N ? so[lane] : N, q.s1 = lane + 64 < N ? so[lane + 64] : N;
-      q.pk0 = piv[min(lane, N - 1)], q.pk1 = piv[min(lane + 64, N - 1)];
-      q.rd0 = 1.0 / (double)A[q.pk0 * lda + min(lane, N - 1)];
-      q.rd1 = 1.0 / (double)A[q.pk1 * lda + min(lane + 64, N - 1)];
-      v0 = lane < N ? b[lane] : 0.0, v1 = lane + 64 < N ? b[lane + 64] : 0.0;
-      lu_solve_regs(A, lda, N, q, v0, v1, lane);
-      if (lane < N) w[q.s0] = v0;
-      if (lane + 64 < N) w[q.s1] = v1;
-    }
-    double dprev = __builtin_inf();
-    for (int it = 0; it < RBF_MAX_REFINE; ++it) {
-      __syncthreads();
-      // v = b − A w in fp64, two threads per row (A recomputed from the coordinates)
-      {
-        const int i = tid >> 1, h = tid & 1;
-        double r = 0.0;
-        if (i < N) {
-          const double xi = xs[i], yi = ys[i];
-          for (int j = h; j < N; j += 2) r = fma(-dist64(xi, yi, xs[j], ys[j]), w[j], r);
-        }
-        r += __shfl_xor(r, 1);
-        if (i < N && h == 0) v[i] = b[i] + r;
-      }
-      __syncthreads();
-      if (wave == 0) {
-        v0 = lane < N ? v[lane] : 0.0, v1 = lane + 64 < N ? v[lane + 64] : 0.0;
-        lu_solve_regs(A, lda, N, q, v0, v1, lane);
-        double dn = 0.0, wn = 0.0;
-        if (lane < N) {
-          const double t = w[q.s0] + v0;
-          w[q.s0] = t;
-          dn = fabs(v0), wn = fabs(t);
-        }
-        if (lane + 64 < N) {
-          const double t = w[q.s1] + v1;
-          w[q.s1] = t;
-          dn = fmax(dn, fabs(v1)), wn = fmax(wn, fabs(t));
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-          dn = fmax(dn, __shfl_xor(dn, off));
-          wn = fmax(wn, __shfl_xor(wn, off));
-        }
-        // remaining error ≈ ρ·dn with ρ = dn / dprev the observed contraction; stop at the
-        // fp64 floor (≈ cond·eps) or when a sweep no longer halves the correction
-        if (lane == 0)
-          s_more = dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
-        dprev = dn;
-      }
-      __syncthreads();
-      if (!s_more) break;  // uniform
-    }
-  }
-  __syncthreads();
-
-  for (int j = tid; j < N; j += 256) {
-    wT[(int64_t)j * P + p] = singular ? __builtin_nan("") : w[j];
-    xyT[(int64_t)j * P + p] = make_float2(lu[base + j], lv[base + j]);
-  }
+  for (int i = 1; i < WAVES; ++i) r = comb<MAX>(r, red[i]);
+  return r;
 }
 
-// ---- 128 < N <= 256: Householder-projected Cholesky in LDS + fp64 refinement --------------
-// An fp32 LU of a 200×200 system no longer fits 160 KiB of LDS (and a 256×256 one is 256 KiB), but
-// the linear-RBF matrix A_ij = ‖x_i − x_j‖ of distinct nodes is symmetric and strictly
-// conditionally negative definite (negative definite on 1^⊥).  With the Householder reflector H
-// that maps e = 1/√N to the last unit vector, HAH = [M m; mᵀ μ] where M (order n = N − 1) is
-// Q̃ᵀAQ̃ on 1^⊥, so S = −M is symmetric positive definite: its fp32 Cholesky factor needs only the
-// packed lower triangle (n(n+1)/2 floats, 127.5 KiB at N = 256).  A w = b is then
-//   c = H b,  z1 = S⁻¹ c₁,  z2 = S⁻¹ m,  y_n = (c_n + mᵀz1)/(μ + mᵀz2),  y₁ = −z1 + z2·y_n,  w = H y
-// (block elimination of the bordered system), used as the approximate inverse of mixed-precision
-// iterative refinement exactly as rbf_solve_lds does: residuals b − A·w in fp64 from the node
-// coordinates, corrections through the fp32 factor, until the fp64 floor (cond·eps), so the result
-// is what SciPy's fp64 LU returns to rounding.  Exactly repeated nodes make A singular (SciPy's
-// LinAlgError): they are detected up front; a Cholesky pivot <= 0 (cond far beyond fp32) reports
-// the same status.
-constexpr int RBF_CH_MAX_N = 256;
-constexpr int RBF_CH_THREADS = 512;
-constexpr int RBF_CH_MAX_REFINE = 16;
-
-__device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower, j <= i
-
-__device__ __forceinline__ double pick4(const double (&v)[4], int q) {
-  return q == 0 ? v[0] : (q == 1 ? v[1] : (q == 2 ? v[2] : v[3]));
-}
-
-__device__ __forceinline__ double wave_sum64(double t) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-  return t;
-}
-
-// v ← S⁻¹ v for S = L Lᵀ (packed fp32 L of order n <= 256) on one wave: lane owns entries
-// lane + 64s; rd[s] = 1 / L_ii for the same entries.  Column-oriented forward then backward
-// substitution; the chain runs through registers (readlane), the next step's factor entries are
-// loaded before the current step's update.  Entries >= n are left unchanged.
-__device__ __forceinline__ void chol_solve(const float* __restrict__ L, int n, const double (&rd)[4], double (&v)[4],
-                                           int lane) {
-  float cur[4], nxt[4];
-  auto fwd_load = [&](int k, float (&dst)[4]) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) dst[s] = L[tri(max(min(lane + 64 * s, n - 1), k), k)];
-  };
-  fwd_load(0, cur);
-  for (int k = 0; k < n; ++k) {
-    if (k + 1 < n) fwd_load(k + 1, nxt);
-    const int q = k >> 6;
-    const double yk = readlane64(pick4(v, q), k & 63) * readlane64(pick4(rd, q), k & 63);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int i = lane + 64 * s;
-      if (i == k) v[s] = yk;
-      else if (i > k && i < n) v[s] = fma(-(double)cur[s], yk, v[s]);
-      cur[s] = nxt[s];
-    }
-  }
-  auto bwd_load = [&](int k, float (&dst)[4]) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) dst[s] = L[tri(k, min(lane + 64 * s, k))];
-  };
-  bwd_load(n - 1, cur);
-  for (int k = n - 1; k >= 0; --k) {
-    if (k > 0) bwd_load(k - 1, nxt);
-    const int q = k >> 6;
-    const double xk = readlane64(pick4(v, q), k & 63) * readlane64(pick4(rd, q), k & 63);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int i = lane + 64 * s;
-      if (i == k) v[s] = xk;
-      else if (i < k) v[s] = fma(-(double)cur[s], xk, v[s]);
-      cur[s] = nxt[s];
-    }
-  }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(RBF_CH_THREADS)
-rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
-               double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+template <int NB, typename T>
+__global__ void __launch_bounds__(NB * NB, 4)
+rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
+              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status, int max_refine) {
+  constexpr int THREADS = NB * NB, WAVES = THREADS / 64, NV = 8 * NB;
+  __shared__ double xs[NV], ys[NV], bv[NV], uv[NV], wv[NV], vv[NV], cv[NV], zv[NV], z2v[NV], mv[NV];
+  __shared__ __attribute__((aligned(16))) float prow[2][NV], pcol[2][NV];
+  __shared__ double red[WAVES];
+  __shared__ int s_flag;
+  const int t = threadIdx.x;
+  const int bi = t / NB, bj = t % NB;
+  const int i0 = 8 * bi, j0 = 8 * bj;
   const int n = N - 1;
-  double* xs = smem;     // [N] nodes (fp64 copies of the fp32 light vectors)
-  double* ys = xs + N;   // [N]
-  double* b = ys + N;    // [N] right-hand side
-  double* w = b + N;     // [N] solution
-  double* v = w + N;     // [N] residual
-  double* g = v + N;     // [N] A·u
-  double* m = g + N;     // [N] (HAH)[·][n]; m[n] = μ
-  float* col = reinterpret_cast<float*>(m + N);  // [N] current Cholesky column
-  float* S = col + ((N + 3) & ~3);                // packed lower triangle of order n
-  __shared__ double s_red;
-  __shared__ int s_flag, s_more;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t p = blockIdx.x;
-  const int64_t base = p * N;
+  const int64_t p = blockIdx.x, base = p * N;
+  const double e = 1.0 / sqrt((double)N), beta = 1.0 / (1.0 - e);  // H = I − β u uᵀ, u = e·1 − e_n
+  auto u = [&](int j) __attribute__((always_inline)) { return j < n ? e : (j == n ? e - 1.0 : 0.0); };
 
-  for (int j = tid; j < N; j += RBF_CH_THREADS) {
-    const float x = lu[base + j], y = lv[base + j];
-    xs[j] = (double)x;
-    ys[j] = (double)y;
-    b[j] = ldd(I + base + j);
-    xyT[(int64_t)j * P + p] = make_float2(x, y);
+  for (int j = t; j < NV; j += THREADS) {
+    float x = 0.f, y = 0.f;
+    double bb = 0.0;
+    if (j < N) {
+      x = lu[base + j], y = lv[base + j], bb = ldd(I + base + j);
+      xyT[(int64_t)j * P + p] = make_float2(x, y);
+    }
+    xs[j] = (double)x, ys[j] = (double)y, bv[j] = bb, uv[j] = u(j);  // SciPy's float64 copies of the nodes
+    wv[j] = vv[j] = cv[j] = zv[j] = z2v[j] = mv[j] = 0.0;  // entries past N take part in block products
+    prow[0][j] = prow[1][j] = pcol[0][j] = pcol[1][j] = 0.f;
   }
-  if (tid == 0) s_flag = 0;
+  if (t == 0) s_flag = 0;
   __syncthreads();
-  // exactly repeated nodes: A has two equal rows (SciPy: LinAlgError)
-  for (int i = wave; i < N; i += RBF_CH_THREADS / 64)
-    for (int j = i + 1 + lane; j < N; j += 64)
-      if (xs[i] == xs[j] && ys[i] == ys[j]) s_flag = 1;
-  // Householder vector u = e − e_n (e = 1/√N), H = I − β u uᵀ, β = 2/uᵀu = 1/(1 − 1/√N)
-  const double e = 1.0 / sqrt((double)N), beta = 1.0 / (1.0 - e);
-  auto u = [&](int i) { return i < n ? e : e - 1.0; };
-  {  // g = A u, two threads per row
-    const int i = tid >> 1, h = tid & 1;
-    double r = 0.0;
-    if (i < N) {
-      const double xi = xs[i], yi = ys[i];
-      for (int j = h; j < N; j += 2) r = fma(dist64(xi, yi, xs[j], ys[j]), u(j), r);
-    }
-    r += __shfl_xor(r, 1);
-    if (i < N && h == 0) g[i] = r;
-  }
-  __syncthreads();
-  if (wave == 0) {
-    double t = 0.0;
-    for (int j = lane; j < N; j += 64) t = fma(u(j), g[j], t);
-    t = wave_sum64(t);
-    if (lane == 0) s_red = t;
-  }
-  __syncthreads();
-  bool singular = s_flag != 0;  // block-uniform
-  if (!singular) {
-    const double sg = s_red, b2 = beta * beta * sg;
-    auto hah = [&](int i, int j) {
-      return dist64(xs[i], ys[i], xs[j], ys[j]) - beta * (u(i) * g[j] + g[i] * u(j)) + b2 * u(i) * u(j);
-    };
-    for (int i = wave; i < n; i += RBF_CH_THREADS / 64)
-      for (int j = lane; j <= i; j += 64) S[tri(i, j)] = (float)(-hah(i, j));
-    for (int i = tid; i < N; i += RBF_CH_THREADS) m[i] = hah(i, n);
-    __syncthreads();
-    // right-looking Cholesky of S: column k scaled, then the trailing triangle updated
-    for (int k = 0; k < n; ++k) {
-      const float dkk = S[tri(k, k)];
-      if (!(dkk > 0.f)) {  // uniform (one LDS word after a barrier)
-        singular = true;
-        break;
-      }
-      const float d = sqrtf(dkk), inv = 1.f / d;
-      for (int i = k + 1 + tid; i < n; i += RBF_CH_THREADS) {
-        const float l = S[tri(i, k)] * inv;
-        S[tri(i, k)] = l;
-        col[i] = l;
-      }
-      __syncthreads();
-      if (tid == 0) S[tri(k, k)] = d;
-      for (int i = k + 1 + wave; i < n; i += RBF_CH_THREADS / 64) {
-        const float li = col[i];
-        float* row = S + tri(i, 0);
-        for (int j = k + 1 + lane; j <= i; j += 64) row[j] = fmaf(-li, col[j], row[j]);
-      }
-      __syncthreads();
-    }
-  }
-  if (!singular) {
-    double rd[4], z2[4], mr[4], wr[4];
-    double mz2 = 0.0, mu = 0.0;
-    if (wave == 0) {
+
+  // out[r] = (A·x)[i0 + r] for x in LDS (zero past N): this thread's 8×8 block of A, reduced over the
+  // block row (lanes bi·NB .. bi·NB + NB − 1).  Rows past N come out as garbage and are never used.
+  // (two passes of 4 rows keep the live fp64 state small next to the 64-register S⁻¹ block)
+  auto a_times = [&](const double* x, double (&out)[8], bool check) __attribute__((always_inline)) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int i = lane + 64 * s;
-        rd[s] = i < n ? 1.0 / (double)S[tri(i, i)] : 0.0;
-        mr[s] = i < n ? m[i] : 0.0;
-        z2[s] = mr[s];
-      }
-      mu = m[n];
-      chol_solve(S, n, rd, z2, lane);
-      double t = 0.0;
+    for (int h = 0; h < 8; h += 4) {
+      double o[4] = {0.0, 0.0, 0.0, 0.0};
+      if (i0 < N && j0 < N) {
+        float xi[4], yi[4];  // the nodes are fp32 values: exact in 32-bit registers
 #pragma unroll
-      for (int s = 0; s < 4; ++s) t = fma(mr[s], z2[s], t);
-      mz2 = wave_sum64(t);
-    }
-    // A⁻¹ r through the bordered Householder system; r: entries lane + 64s (wave 0)
-    auto solve = [&](double (&r)[4]) {
-      double t = 0.0;
+        for (int r = 0; r < 4; ++r)
+          xi[r] = (float)xs[min(i0 + h + r, N - 1)], yi[r] = (float)ys[min(i0 + h + r, N - 1)];
+#pragma unroll 1
+        for (int c = 0; c < 8; ++c) {  // not unrolled: 32 fp64 sqrt chains in flight would evict S⁻¹
+          const double xc = xs[j0 + c], yc = ys[j0 + c], xj = x[j0 + c];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) t = fma(lane + 64 * s < N ? u(lane + 64 * s) : 0.0, r[s], t);
-      const double ub = wave_sum64(t);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int i = lane + 64 * s;
-        r[s] = i < N ? fma(-beta * u(i), ub, r[s]) : 0.0;  // c = H r
-      }
-      const double cn = readlane64(pick4(r, n >> 6), n & 63);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (lane + 64 * s >= n) r[s] = 0.0;
-      chol_solve(S, n, rd, r, lane);  // z1
-      t = 0.0;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t = fma(mr[s], r[s], t);
-      const double yn = (cn + wave_sum64(t)) / (mu + mz2);
-      t = 0.0;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int i = lane + 64 * s;
-        r[s] = i < n ? fma(z2[s], yn, -r[s]) : (i == n ? yn : 0.0);
-        t = fma(i < N ? u(i) : 0.0, r[s], t);
-      }
-      const double uy = wave_sum64(t);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int i = lane + 64 * s;
-        if (i < N) r[s] = fma(-beta * u(i), uy, r[s]);  // w = H y
-      }
-    };
-    if (wave == 0) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) wr[s] = lane + 64 * s < N ? b[lane + 64 * s] : 0.0;
-      solve(wr);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (lane + 64 * s < N) w[lane + 64 * s] = wr[s];
-    }
-    double dprev = __builtin_inf();
-    for (int it = 0; it < RBF_CH_MAX_REFINE; ++it) {
-      __syncthreads();
-      {  // v = b − A w in fp64, two threads per row
-        const int i = tid >> 1, h = tid & 1;
-        double r = 0.0;
-        if (i < N) {
-          const double xi = xs[i], yi = ys[i];
-          for (int j = h; j < N; j += 2) r = fma(-dist64(xi, yi, xs[j], ys[j]), w[j], r);
-        }
-        r += __shfl_xor(r, 1);
-        if (i < N && h == 0) v[i] = b[i] + r;
-      }
-      __syncthreads();
-      if (wave == 0) {
-        double dv[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) dv[s] = lane + 64 * s < N ? v[lane + 64 * s] : 0.0;
-        solve(dv);
-        double dn = 0.0, wn = 0.0;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int i = lane + 64 * s;
-          if (i < N) {
-            wr[s] += dv[s];
-            w[i] = wr[s];
-            dn = fmax(dn, fabs(dv[s]));
-            wn = fmax(wn, fabs(wr[s]));
+          for (int r = 0; r < 4; ++r) {
+            o[r] = fma(dist64((double)xi[r], (double)yi[r], xc, yc), xj, o[r]);
+            if (check && i0 + h + r < N && j0 + c < N && i0 + h + r != j0 + c && (double)xi[r] == xc &&
+                (double)yi[r] == yc)
+              s_flag = 1;
           }
         }
+      }
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-          dn = fmax(dn, __shfl_xor(dn, off));
-          wn = fmax(wn, __shfl_xor(wn, off));
-        }
-        if (lane == 0)
-          s_more = dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
-        dprev = dn;
+      for (int r = 0; r < 4; ++r) out[h + r] = row_sum<NB>(o[r]);
+    }
+  };
+  double part[8];
+  a_times(uv, part, true);  // g = A u, and the repeated-node check
+  if (bj == 0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      if (i0 + r < N) vv[i0 + r] = part[r];
+  }
+  __syncthreads();
+  const double sg = block_reduce<WAVES, false>(t < N ? u(t) * vv[t] : 0.0, red);  // uᵀAu
+  const double b2 = beta * beta * sg;
+  auto hah = [&](int i, int j) __attribute__((always_inline)) {
+    return dist64(xs[i], ys[i], xs[j], ys[j]) - beta * (u(i) * vv[j] + vv[i] * u(j)) + b2 * u(i) * u(j);
+  };
+  float a[8][8];  // the thread's 8×8 block of S (rows i0.., columns j0..)
+  const int nb = (n + 7) >> 3;
+  const bool live = bi < nb && bj < nb;
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) a[r][c] = (live && i0 + r < n && j0 + c < n) ? (float)(-hah(i0 + r, j0 + c)) : 0.f;
+  if (t <= n) mv[t] = hah(t, n);  // m, and μ at n
+  bool singular = s_flag != 0;  // written before the reduction's barriers: block-uniform
+  __syncthreads();
+
+  // Step k = 8·kb + KR: KR is a compile-time constant (the step loop is unrolled by 8), so the pivot
+  // row and column are fixed registers of the owning threads.
+  auto step = [&](auto KRc, int kb) __attribute__((always_inline)) -> bool {
+    constexpr int KR = decltype(KRc)::value;
+    const int k = 8 * kb + KR, buf = KR & 1;
+    if (bi == kb) {  // publish row k (this thread's 8 columns of it)
+      *reinterpret_cast<float4*>(&prow[buf][j0]) = make_float4(a[KR][0], a[KR][1], a[KR][2], a[KR][3]);
+      *reinterpret_cast<float4*>(&prow[buf][j0 + 4]) = make_float4(a[KR][4], a[KR][5], a[KR][6], a[KR][7]);
+    }
+    if (bj == kb) {  // publish column k
+      *reinterpret_cast<float4*>(&pcol[buf][i0]) = make_float4(a[0][KR], a[1][KR], a[2][KR], a[3][KR]);
+      *reinterpret_cast<float4*>(&pcol[buf][i0 + 4]) = make_float4(a[4][KR], a[5][KR], a[6][KR], a[7][KR]);
+    }
+    __syncthreads();
+    const float piv = pcol[buf][k];
+    if (!(piv > 0.f)) return false;  // block-uniform (one LDS word after the barrier)
+    const float inv = 1.f / piv;
+    if (live) {
+      const float4 r0 = *reinterpret_cast<const float4*>(&prow[buf][j0]);
+      const float4 r1 = *reinterpret_cast<const float4*>(&prow[buf][j0 + 4]);
+      const float4 c0 = *reinterpret_cast<const float4*>(&pcol[buf][i0]);
+      const float4 c1 = *reinterpret_cast<const float4*>(&pcol[buf][i0 + 4]);
+      const float pr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+      const float d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      // One FMA pass does the whole step: with â_kk := 1 + 1/a_kk the pivot column comes out as
+      // a_ik − a_ik(1 + 1/a_kk) = −a_ik/a_kk, and with the pivot row's multiplier a_kk − 1 the pivot
+      // row comes out as a_kj − (a_kk − 1)·a_kj/a_kk = a_kj/a_kk (and 1/a_kk on the diagonal)
+      float rf[8], dm[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) rf[c] = (c == KR && bj == kb) ? 1.f + inv : pr[c] * inv;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) dm[r] = (r == KR && bi == kb) ? d[r] - 1.f : d[r];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) a[r][c] = fmaf(-dm[r], rf[c], a[r][c]);
+    }
+    return true;
+  };
+  using std::integral_constant;
+  for (int kb = 0; kb < nb && !singular; ++kb) {
+    // steps past n - 1 are skipped (uniform); the LDS buffers alternate with KR's parity, so two
+    // consecutive steps never share one (the barrier of step k orders the reads of step k - 2)
+    singular = !step(integral_constant<int, 0>(), kb);
+    if (!singular && 8 * kb + 1 < n) singular = !step(integral_constant<int, 1>(), kb);
+    if (!singular && 8 * kb + 2 < n) singular = !step(integral_constant<int, 2>(), kb);
+    if (!singular && 8 * kb + 3 < n) singular = !step(integral_constant<int, 3>(), kb);
+    if (!singular && 8 * kb + 4 < n) singular = !step(integral_constant<int, 4>(), kb);
+    if (!singular && 8 * kb + 5 < n) singular = !step(integral_constant<int, 5>(), kb);
+    if (!singular && 8 * kb + 6 < n) singular = !step(integral_constant<int, 6>(), kb);
+    if (!singular && 8 * kb + 7 < n) singular = !step(integral_constant<int, 7>(), kb);
+  }
+
+  double w_t = 0.0;
+  if (!singular) {
+    // dst[i0 + r] = (S⁻¹·x)[i0 + r] for x in LDS; entries of S⁻¹ past n are zero
+    auto sinv_times = [&](const double* x, double* dst) __attribute__((always_inline)) {
+      double out[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) out[r] = 0.0;
+      if (live) {
+        double xj[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) xj[c] = x[j0 + c];
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            // opaque to the optimizer: hoisting the 64 fp64 conversions out of the refinement loop
+            // would need 128 live registers and spill S⁻¹ itself
+            asm volatile("" : "+v"(a[r][c]));
+            out[r] = fma((double)a[r][c], xj[c], out[r]);
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) out[r] = row_sum<NB>(out[r]);
+      if (bj == 0) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (i0 + r < n) dst[i0 + r] = out[r];
       }
       __syncthreads();
-      if (!s_more) break;  // uniform
+    };
+    sinv_times(mv, z2v);  // z2 = S⁻¹ m
+    const double mu = mv[n];
+    const double mz2 = block_reduce<WAVES, false>(t < n ? mv[t] * z2v[t] : 0.0, red);
+    // A⁻¹ r for r in LDS, through the bordered Householder system; thread t returns entry t (< N)
+    auto solve = [&](const double* rv) __attribute__((always_inline)) {
+      const double ub = block_reduce<WAVES, false>(t < N ? u(t) * rv[t] : 0.0, red);
+      if (t < N) cv[t] = fma(-beta * u(t), ub, rv[t]);  // c = H r
+      __syncthreads();
+      const double cn = cv[n];
+      sinv_times(cv, zv);  // z1 = S⁻¹ c₁ (entries of S⁻¹ in column n are zero, so c_n drops out)
+      const double mz1 = block_reduce<WAVES, false>(t < n ? mv[t] * zv[t] : 0.0, red);
+      const double yn = (cn + mz1) / (mu + mz2);
+      const double y = t < n ? fma(z2v[t], yn, -zv[t]) : (t == n ? yn : 0.0);
+      const double uy = block_reduce<WAVES, false>(t < N ? u(t) * y : 0.0, red);
+      return fma(-beta * u(t), uy, y);  // w = H y
+    };
+    w_t = solve(bv);
+    if (t < N) wv[t] = w_t;
+    double dprev = __builtin_inf();
+    const int sweeps = max_refine < 0 ? -max_refine : max_refine;  // < 0: exactly that many (measurement)
+    for (int it = 0; it < sweeps; ++it) {
+      __syncthreads();
+      a_times(wv, part, false);  // v = b − A w in fp64
+      if (bj == 0) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (i0 + r < N) vv[i0 + r] = bv[i0 + r] - part[r];
+      }
+      __syncthreads();
+      const double dv = solve(vv);
+      double dn = 0.0, wn = 0.0;
+      if (t < N) {
+        w_t += dv;
+        wv[t] = w_t;
+        dn = fabs(dv), wn = fabs(w_t);
+      }
+      dn = block_reduce<WAVES, true>(dn, red);
+      wn = block_reduce<WAVES, true>(wn, red);
+      // remaining error ≈ ρ·dn with ρ = dn / dprev the observed contraction (rbf_solve_lds's rule)
+      const bool more =
+          dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
+      dprev = dn;
+      if (!more && it >= 2 && max_refine >= 0) break;  // uniform: every thread computed the same reductions
     }
   }
-  if (singular && tid == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
-  __syncthreads();
-  for (int j = tid; j < N; j += RBF_CH_THREADS) wT[(int64_t)j * P + p] = singular ? __builtin_nan("") : w[j];
-}
-
-size_t rbf_chol_lds(int N) {
-  const int n = N - 1;
-  return 7 * (size_t)N * sizeof(double) + (size_t)((N + 3) & ~3) * sizeof(float) +
-         (size_t)n * (n + 1) / 2 * sizeof(float);
+  if (singular && t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
+  if (t < N) wT[(int64_t)t * P + p] = singular ? __builtin_nan("") : w_t;
 }
 
 // Wave-wide max of a u32 key: DPP within each row of 16 lanes, then the four row maxima
@@ -582,7 +360,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return max(max(r0, r1), max(r2, r3));
 }
 
-// Per-pixel solve for N ≤ NMAX ≤ 112: Gauss-Jordan elimination with partial pivoting in
+// Per-pixel solve for N ≤ NMAX ≤ 80: Gauss-Jordan elimination with partial pivoting in
 // fp64 registers (what SciPy's gesv computes, to rounding: cond·eps ≈ 1e-12 relative).
 //
 // One workgroup per pixel, one thread per row: thread t holds row t of [A | b] in
@@ -747,14 +525,39 @@ rbf_eval(const double* __restrict__ wT, const float2* __restrict__ xyT, int N, i
   }
 }
 
-constexpr int RBF_GJ_MAX_N = 112;
+// fp64 register Gauss-Jordan up to here, rbf_solve_gji above (solve of a 400×400 ROI, MI355X:
+// N = 64: 6.3 vs 13.2 ms, N = 96: 27.9 vs 18.1 ms; tools/time_rbf_solve.py)
+constexpr int RBF_GJ_MAX_N = 80;
 constexpr int RBF_TE = 20;  // divides the reference's 100-wide grid rows (shared qv)
+
+// Measurement overrides (environment, read once): RTI_RBF_GJI_MIN_N lowers the smallest N solved by
+// rbf_solve_gji, RTI_RBF_GJI_REFINE = its refinement sweep cap (< 0: exactly that many sweeps).
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+int gji_min_n() {
+  static const int v = env_int("RTI_RBF_GJI_MIN_N", RBF_GJ_MAX_N + 1);
+  return v;
+}
+int gji_refine() {
+  static const int v = env_int("RTI_RBF_GJI_REFINE", RBF_GJI_MAX_REFINE);
+  return v;
+}
 
 template <typename T>
 void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
                   int* status, hipStream_t s) {
   const T* In = static_cast<const T*>(I);
   const dim3 g((unsigned)P);
+  if (N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n())) {
+    if (N <= 128)
+      hipLaunchKernelGGL((rbf_solve_gji<16, T>), g, dim3(256), 0, s, lu, lv, In, N, P, wT, xyT, status, gji_refine());
+    else
+      hipLaunchKernelGGL((rbf_solve_gji<32, T>), g, dim3(1024), 0, s, lu, lv, In, N, P, wT, xyT, status,
+                         gji_refine());
+    return;
+  }
 #define RBF_GJ(NM)                                                                                       \
   hipLaunchKernelGGL((rbf_solve_gj<NM, T>), g, dim3(GjSolve<NM, T>::THREADS), 0, s, lu, lv, In, N, P, wT, \
                      xyT, status)
@@ -762,21 +565,7 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
   else if (N <= 32) RBF_GJ(32);
   else if (N <= 48) RBF_GJ(48);
   else if (N <= 64) RBF_GJ(64);
-  else if (N <= 80) RBF_GJ(80);
-  else if (N <= 96) RBF_GJ(96);
-  else if (N <= RBF_GJ_MAX_N) RBF_GJ(112);
-  else if (N > RBF_MAX_N) {
-    const size_t lds = rbf_chol_lds(N);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rbf_solve_chol<T>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((rbf_solve_chol<T>), g, dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status);
-  } else {
-    const size_t lds = 5 * (size_t)N * sizeof(double) + 2 * (size_t)N * sizeof(int) + (size_t)N * ((N + 2) & ~1) * sizeof(float);
-    if (lds > 65536)  // opt in to more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rbf_solve_lds<T>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((rbf_solve_lds<T>), g, dim3(256), lds, s, lu, lv, In, N, P, wT, xyT, status);
-  }
+  else RBF_GJ(80);
 #undef RBF_GJ
 }
 
@@ -803,7 +592,7 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
                                 rti_stream_t stream) {
   if (!lu || !lv || !I || !luv || !out || !status) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: null pointer");
   if (N <= 0 || P <= 0 || E <= 0) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: N, P, E must be positive");
-  if (N > RBF_CH_MAX_N) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: N=%d > %d lights", N, RBF_CH_MAX_N);
+  if (N > RBF_MAX_N) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: N=%d > %d lights", N, RBF_MAX_N);
   if (P > 0x7fffffff) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: P too large for one launch");
   if (in_dtype != RTI_F32 && in_dtype != RTI_U8 && in_dtype != RTI_I32)
     return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: input dtype %d", in_dtype);

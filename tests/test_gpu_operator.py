@@ -165,11 +165,12 @@ def test_compat_default_interpolation_perpixel(cuda):
         compat.interpolate_intensities((d["singular_lx"], d["singular_ly"], d["I"][:1, :1]))
 
 
-@pytest.mark.parametrize("n", [6, 37, 64, 65, 100, 112, 113, 128, 129, 160, 200, 255, 256])
+@pytest.mark.parametrize("n", [2, 6, 37, 64, 65, 80, 81, 100, 127, 128, 129, 160, 200, 255, 256])
 def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
-    """Every solver of rti_rbf_perpixel: register Gauss-Jordan (N <= 112), fp32 LU in LDS (<= 128),
-    Householder-projected Cholesky (<= 256; SURVEY §6 timed the reference at N = 200), each with the
-    reference's per-pixel geometry, against SciPy's fp64 solve restated in the oracle."""
+    """Every solver of rti_rbf_perpixel: fp64 register Gauss-Jordan (N <= 80) and the register-blocked
+    fp32 Gauss-Jordan inverse + fp64 refinement on 16x16 (N <= 128) and 32x32 (N <= 256) block
+    grids (SURVEY §6 timed the reference at N = 200), each with the reference's per-pixel geometry,
+    against SciPy's fp64 solve restated in the oracle."""
     ys, xs = np.mgrid[0:3, 0:5]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
@@ -182,10 +183,10 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     assert ok, err
 
 
-@pytest.mark.parametrize("n", [129, 200, 256])
+@pytest.mark.parametrize("n", [81, 128, 129, 200, 256])
 def test_rbf_perpixel_large_n_repeated_node_raises(cuda, n):
     """A repeated light direction makes A exactly singular: SciPy raises LinAlgError; so does the
-    N > 128 solver; N > 256 is refused (RTI_ERR_UNSUPPORTED)."""
+    block Gauss-Jordan solver; N > 256 is refused (RTI_ERR_UNSUPPORTED)."""
     ys, xs = np.mgrid[0:2, 0:2]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
