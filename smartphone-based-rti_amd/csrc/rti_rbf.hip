@@ -232,7 +232,7 @@ rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const 
     __syncthreads();
     const float piv = pcol[buf][k];
     if (!(piv > 0.f)) return false;  // block-uniform (one LDS word after the barrier)
-    const float inv = 1.f / piv;
+    const float inv = __builtin_amdgcn_rcpf(piv);  // an approximate inverse is all the refinement needs
     if (live) {
       const float4 r0 = *reinterpret_cast<const float4*>(&prow[buf][j0]);
       const float4 r1 = *reinterpret_cast<const float4*>(&prow[buf][j0 + 4]);
@@ -243,15 +243,17 @@ rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const 
       // One FMA pass does the whole step: with â_kk := 1 + 1/a_kk the pivot column comes out as
       // a_ik − a_ik(1 + 1/a_kk) = −a_ik/a_kk, and with the pivot row's multiplier a_kk − 1 the pivot
       // row comes out as a_kj − (a_kk − 1)·a_kj/a_kk = a_kj/a_kk (and 1/a_kk on the diagonal)
-      float rf[8], dm[8];
+      float nrf[8], dm[8];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) rf[c] = (c == KR && bj == kb) ? 1.f + inv : pr[c] * inv;
+      for (int c = 0; c < 8; ++c) nrf[c] = pr[c] * -inv;
+      if (bj == kb) nrf[KR] = -(1.f + inv);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) dm[r] = (r == KR && bi == kb) ? d[r] - 1.f : d[r];
+      for (int r = 0; r < 8; ++r) dm[r] = d[r];
+      if (bi == kb) dm[KR] = d[KR] - 1.f;
 #pragma unroll
       for (int r = 0; r < 8; ++r)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) a[r][c] = fmaf(-dm[r], rf[c], a[r][c]);
+        for (int c = 0; c < 8; ++c) a[r][c] = fmaf(dm[r], nrf[c], a[r][c]);
     }
     return true;
   };
@@ -338,6 +340,251 @@ rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const 
       dn = block_reduce<WAVES, true>(dn, red);
       wn = block_reduce<WAVES, true>(wn, red);
       // remaining error ≈ ρ·dn with ρ = dn / dprev the observed contraction (rbf_solve_lds's rule)
+      const bool more =
+          dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
+      dprev = dn;
+      if (!more && it >= 2 && max_refine >= 0) break;  // uniform: every thread computed the same reductions
+    }
+  }
+  if (singular && t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
+  if (t < N) wT[(int64_t)t * P + p] = singular ? __builtin_nan("") : w_t;
+}
+
+// Lower-triangle form (the kernel below): the in-place Gauss-Jordan sweep keeps the matrix symmetric up to
+// sign — after steps 0..k−1, a_ij = a_ji when i and j are both swept or both not, a_ij = −a_ji when
+// exactly one is — so only the blocks (bi, bj) with bj ≤ bi are held (diagonal blocks whole), one
+// thread per block: nb(nb+1)/2 threads for nb = ⌈n/8⌉ (325 at N = 200 against 625 for the full grid).
+// Step k needs only the column v = a_·k: rows ≥ 8⌊k/8⌋ come from the block column ⌊k/8⌋, rows above
+// it from block row ⌊k/8⌋ as −a_kx (k unswept, x swept), and row k is a_kj = ±v_j (− for j < k).
+// Products with the symmetric S⁻¹ and A use each off-diagonal block twice (its rows and, transposed,
+// its columns); the partial sums land in an LDS table P[column block][row], every (block, row) slot
+// written exactly once, and each row adds its slots in a fixed order (deterministic).
+// 8 waves, 512 blocks: ⌈N/8⌉ ≤ 31 block rows of A, N ≤ 248, with the 256-VGPR budget of 2 waves per
+// SIMD (no spills).  N ≤ 128 and N = 249..256 take rbf_solve_gji's full grid (for N ≤ 128 its
+// 256-thread workgroups, four per CU, beat this kernel's: 20–24 vs 31 ms at N = 100).
+template <int NB>
+struct GjsShape {
+  static constexpr int NV = 8 * NB;                              // vector capacity
+  static constexpr int BLOCKS = NB * (NB + 1) / 2;
+  static constexpr int THREADS = BLOCKS > 512 ? 512 : (BLOCKS + 63) / 64 * 64;
+  static constexpr int WAVES = THREADS / 64;
+  static constexpr int MIN_WAVES = 2;                            // VGPR cap 256 (no spills)
+  static constexpr int MAX_N = NB <= 16 ? 128 : 248;
+};
+
+template <int NB, typename T>
+__global__ void __launch_bounds__(GjsShape<NB>::THREADS, GjsShape<NB>::MIN_WAVES)
+rbf_solve_gjs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
+              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status, int max_refine) {
+  using SH = GjsShape<NB>;
+  constexpr int THREADS = SH::THREADS, WAVES = SH::WAVES, NV = SH::NV;
+  __shared__ double xs[NV], ys[NV], bv[NV], uv[NV], wv[NV], vv[NV], cv[NV], zv[NV], z2v[NV], mv[NV];
+  __shared__ double Pt[NB][NV];  // partial products: Pt[column block][row]
+  __shared__ __attribute__((aligned(16))) float vcol[2][NV];
+  __shared__ double red[WAVES];
+  __shared__ int s_flag;
+  const int t = threadIdx.x;
+  int bi = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);  // t = bi(bi+1)/2 + bj, bj <= bi
+  if ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+  if (bi * (bi + 1) / 2 > t) --bi;
+  const int bj = t - bi * (bi + 1) / 2;
+  const int i0 = 8 * bi, j0 = 8 * bj;
+  const bool diag = bi == bj;
+  const int n = N - 1;
+  const int nb = (n + 7) >> 3, nbA = (N + 7) >> 3;        // block rows of S and of A
+  const bool liveS = t < nb * (nb + 1) / 2, liveA = t < nbA * (nbA + 1) / 2;
+  const int64_t p = blockIdx.x, base = p * N;
+  const double e = 1.0 / sqrt((double)N), beta = 1.0 / (1.0 - e);  // H = I − β u uᵀ, u = e·1 − e_n
+  auto u = [&](int j) __attribute__((always_inline)) { return j < n ? e : (j == n ? e - 1.0 : 0.0); };
+
+  for (int j = t; j < NV; j += THREADS) {
+    float x = 0.f, y = 0.f;
+    double bb = 0.0;
+    if (j < N) {
+      x = lu[base + j], y = lv[base + j], bb = ldd(I + base + j);
+      xyT[(int64_t)j * P + p] = make_float2(x, y);
+    }
+    xs[j] = (double)x, ys[j] = (double)y, bv[j] = bb, uv[j] = u(j);  // SciPy's float64 copies of the nodes
+    wv[j] = vv[j] = cv[j] = zv[j] = z2v[j] = mv[j] = 0.0;  // entries past N take part in block products
+    vcol[0][j] = vcol[1][j] = 0.f;
+  }
+  if (t == 0) s_flag = 0;
+  __syncthreads();
+
+  // dst[x] = Σ_y M_xy src[y] for symmetric M given by this thread's lower block (element (r, c) =
+  // elem(r, c), rows i0.., columns j0..), for x < len; src zero past its length.  Ends with a barrier.
+  // REG: elem reads the register block (columns unrolled: compile-time indices); otherwise elem
+  // computes A's entries (columns not unrolled: 32 fp64 sqrt chains in flight would evict S⁻¹).
+  auto sym_times = [&](const double* src, double* dst, int len, bool live, auto elem, auto REG)
+                       __attribute__((always_inline)) {
+    if (live) {
+#pragma unroll
+      for (int h = 0; h < 8; h += 4) {  // two passes of 4 rows: little fp64 state next to the S⁻¹ block
+        double xr[4], rp[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xr[r] = src[i0 + h + r], rp[r] = 0.0;
+        auto col = [&](int c) __attribute__((always_inline)) {
+          const double xc = src[j0 + c];
+          double cc = 0.0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double m = elem(h + r, c);
+            rp[r] = fma(m, xc, rp[r]);
+            cc = fma(m, xr[r], cc);
+          }
+          if (!diag) Pt[bi][j0 + c] = h ? Pt[bi][j0 + c] + cc : cc;  // this thread's slot
+        };
+        if constexpr (decltype(REG)::value) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) col(c);
+        } else {
+#pragma unroll 1
+          for (int c = 0; c < 8; ++c) col(c);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Pt[bj][i0 + h + r] = rp[r];
+      }
+    }
+    __syncthreads();
+    const int nbl = (len + 7) >> 3;
+    for (int x = t; x < len; x += THREADS) {
+      double sacc = 0.0;
+      for (int cb = 0; cb < nbl; ++cb) sacc += Pt[cb][x];
+      dst[x] = sacc;
+    }
+    __syncthreads();
+  };
+  // A's entries from the node coordinates (correctly rounded fp64 sqrt: pdist's values)
+  auto a_elem = [&](int r, int c) __attribute__((always_inline)) {
+    return dist64(xs[i0 + r], ys[i0 + r], xs[j0 + c], ys[j0 + c]);
+  };
+  if (liveA) {  // repeated nodes: A singular (SciPy: LinAlgError)
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (i0 + r < N && j0 + c < N && i0 + r != j0 + c && xs[i0 + r] == xs[j0 + c] && ys[i0 + r] == ys[j0 + c])
+          s_flag = 1;
+  }
+  sym_times(uv, vv, N, liveA, a_elem, std::false_type());  // g = A u
+  const double sg = block_reduce<WAVES, false>(t < N ? u(t) * vv[t] : 0.0, red);  // uᵀAu
+  const double b2 = beta * beta * sg;
+  auto hah = [&](int i, int j) __attribute__((always_inline)) {
+    return dist64(xs[i], ys[i], xs[j], ys[j]) - beta * (u(i) * vv[j] + vv[i] * u(j)) + b2 * u(i) * u(j);
+  };
+  float a[8][8];  // this thread's lower block of S
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) a[r][c] = (liveS && i0 + r < n && j0 + c < n) ? (float)(-hah(i0 + r, j0 + c)) : 0.f;
+  if (t <= n) mv[t] = hah(t, n);  // m, and μ at n
+  bool singular = s_flag != 0;  // set before the reduction's barriers: block-uniform
+  __syncthreads();
+
+  // Step k = 8·kb + KR (KR compile-time: the loop is unrolled by 8, so the pivot row/column is a fixed
+  // register set of its owners).  vcol alternates with KR's parity; the barrier of step k orders the
+  // reads of step k − 2.
+  auto step = [&](auto KRc, int kb) __attribute__((always_inline)) {
+    constexpr int KR = decltype(KRc)::value;
+    const int k = 8 * kb + KR;
+    if (k >= n) return;  // uniform
+    float* v = vcol[KR & 1];
+    if (liveS && bi == kb && !diag) {  // rows x < 8kb of column k: −a_kx (row KR of block (kb, bj))
+      *reinterpret_cast<float4*>(&v[j0]) = make_float4(-a[KR][0], -a[KR][1], -a[KR][2], -a[KR][3]);
+      *reinterpret_cast<float4*>(&v[j0 + 4]) = make_float4(-a[KR][4], -a[KR][5], -a[KR][6], -a[KR][7]);
+    }
+    if (liveS && bj == kb) {  // rows x >= 8kb: column KR of block (bi, kb), the diagonal block whole
+      *reinterpret_cast<float4*>(&v[i0]) = make_float4(a[0][KR], a[1][KR], a[2][KR], a[3][KR]);
+      *reinterpret_cast<float4*>(&v[i0 + 4]) = make_float4(a[4][KR], a[5][KR], a[6][KR], a[7][KR]);
+    }
+    __syncthreads();
+    const float piv = v[k];
+    const bool bad = !(piv > 0.f);  // block-uniform (one LDS word after the barrier)
+    singular |= bad;  // no early exit: a straight-line step keeps the block in registers
+    // an approximate reciprocal is enough: the inverse only has to be a good approximate inverse
+    const float inv = __builtin_amdgcn_rcpf(piv);
+    if (liveS && !bad) {
+      const float4 q0 = *reinterpret_cast<const float4*>(&v[j0]);
+      const float4 q1 = *reinterpret_cast<const float4*>(&v[j0 + 4]);
+      const float4 c0 = *reinterpret_cast<const float4*>(&v[i0]);
+      const float4 c1 = *reinterpret_cast<const float4*>(&v[i0 + 4]);
+      const float vj[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+      const float vi[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      // one FMA pass: row k is a_kj = ±v_j (− where j is swept: j < k), and with â_kk := 1 + 1/a_kk and
+      // the pivot row's multiplier a_kk − 1 the pivot column and row come out as −a_ik/a_kk and
+      // a_kj/a_kk.  j < k is bj ≤ kb for the columns c < KR of a block and bj < kb for c ≥ KR, so the
+      // signs cost two selects per step; the FMA takes the negated row factor.
+      const float nlo = bj <= kb ? inv : -inv, nhi = bj < kb ? inv : -inv;  // −(sign · 1/a_kk)
+      float nrf[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) nrf[c] = vj[c] * (c < KR ? nlo : nhi);
+      if (bj == kb) nrf[KR] = -(1.f + inv);
+      float dm[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) dm[r] = vi[r];
+      if (bi == kb) dm[KR] = vi[KR] - 1.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) a[r][c] = fmaf(dm[r], nrf[c], a[r][c]);
+    }
+  };
+  using std::integral_constant;
+  for (int kb = 0; kb < nb && !singular; ++kb) {
+    step(integral_constant<int, 0>(), kb);
+    step(integral_constant<int, 1>(), kb);
+    step(integral_constant<int, 2>(), kb);
+    step(integral_constant<int, 3>(), kb);
+    step(integral_constant<int, 4>(), kb);
+    step(integral_constant<int, 5>(), kb);
+    step(integral_constant<int, 6>(), kb);
+    step(integral_constant<int, 7>(), kb);
+  }
+
+  double w_t = 0.0;
+  if (!singular) {
+    // S⁻¹ (all of 0..n−1 swept: symmetric again); the asm makes each entry opaque so the 64 fp64
+    // conversions are not hoisted out of the refinement loop (128 live registers would spill S⁻¹)
+    auto s_elem = [&](int r, int c) __attribute__((always_inline)) {
+      float x = a[r][c];
+      asm volatile("" : "+v"(x));
+      return (double)x;
+    };
+    sym_times(mv, z2v, n, liveS, s_elem, std::true_type());  // z2 = S⁻¹ m (μ at n meets a zero column)
+    const double mu = mv[n];
+    const double mz2 = block_reduce<WAVES, false>(t < n ? mv[t] * z2v[t] : 0.0, red);
+    // A⁻¹ r for r in LDS, through the bordered Householder system; thread t returns entry t (< N)
+    auto solve = [&](const double* rv) __attribute__((always_inline)) {
+      const double ub = block_reduce<WAVES, false>(t < N ? u(t) * rv[t] : 0.0, red);
+      if (t < N) cv[t] = fma(-beta * u(t), ub, rv[t]);  // c = H r
+      __syncthreads();
+      const double cn = cv[n];
+      sym_times(cv, zv, n, liveS, s_elem, std::true_type());  // z1 = S⁻¹ c₁ (c_n meets S⁻¹'s zero column n)
+      const double mz1 = block_reduce<WAVES, false>(t < n ? mv[t] * zv[t] : 0.0, red);
+      const double yn = (cn + mz1) / (mu + mz2);
+      const double y = t < n ? fma(z2v[t], yn, -zv[t]) : (t == n ? yn : 0.0);
+      const double uy = block_reduce<WAVES, false>(t < N ? u(t) * y : 0.0, red);
+      return fma(-beta * u(t), uy, y);  // w = H y
+    };
+    w_t = solve(bv);
+    if (t < N) wv[t] = w_t;
+    __syncthreads();
+    double dprev = __builtin_inf();
+    const int sweeps = max_refine < 0 ? -max_refine : max_refine;  // < 0: exactly that many (measurement)
+    for (int it = 0; it < sweeps; ++it) {
+      sym_times(wv, vv, N, liveA, a_elem, std::false_type());  // A w in fp64
+      if (t < N) vv[t] = bv[t] - vv[t];
+      __syncthreads();
+      const double dv = solve(vv);
+      double dn = 0.0, wn = 0.0;
+      if (t < N) {
+        w_t += dv;
+        wv[t] = w_t;
+        dn = fabs(dv), wn = fabs(w_t);
+      }
+      dn = block_reduce<WAVES, true>(dn, red);
+      wn = block_reduce<WAVES, true>(wn, red);
+      // remaining error ≈ ρ·dn with ρ = dn / dprev the observed contraction; at least 3 sweeps
       const bool more =
           dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
       dprev = dn;
@@ -553,6 +800,9 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
   if (N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n())) {
     if (N <= 128)
       hipLaunchKernelGGL((rbf_solve_gji<16, T>), g, dim3(256), 0, s, lu, lv, In, N, P, wT, xyT, status, gji_refine());
+    else if (N <= GjsShape<32>::MAX_N)
+      hipLaunchKernelGGL((rbf_solve_gjs<32, T>), g, dim3(GjsShape<32>::THREADS), 0, s, lu, lv, In, N, P, wT, xyT,
+                         status, gji_refine());
     else
       hipLaunchKernelGGL((rbf_solve_gji<32, T>), g, dim3(1024), 0, s, lu, lv, In, N, P, wT, xyT, status,
                          gji_refine());

@@ -165,12 +165,13 @@ def test_compat_default_interpolation_perpixel(cuda):
         compat.interpolate_intensities((d["singular_lx"], d["singular_ly"], d["I"][:1, :1]))
 
 
-@pytest.mark.parametrize("n", [2, 6, 37, 64, 65, 80, 81, 100, 127, 128, 129, 160, 200, 255, 256])
+@pytest.mark.parametrize("n", [2, 6, 37, 64, 65, 80, 81, 100, 127, 128, 129, 160, 200, 248, 249, 255, 256])
 def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     """Every solver of rti_rbf_perpixel: fp64 register Gauss-Jordan (N <= 80) and the register-blocked
-    fp32 Gauss-Jordan inverse + fp64 refinement on 16x16 (N <= 128) and 32x32 (N <= 256) block
-    grids (SURVEY §6 timed the reference at N = 200), each with the reference's per-pixel geometry,
-    against SciPy's fp64 solve restated in the oracle."""
+    fp32 Gauss-Jordan inverse + fp64 refinement on the full 16x16 block grid (N <= 128), the
+    lower-triangle block grid (N <= 248) and the full 32x32 grid (N <= 256) (SURVEY §6 timed the
+    reference at N = 200), each with the reference's per-pixel geometry, against SciPy's fp64 solve
+    restated in the oracle."""
     ys, xs = np.mgrid[0:3, 0:5]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
