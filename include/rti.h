@@ -231,8 +231,10 @@ int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp,
 /* ---- device: per-pixel linear RBF (the reference's default, with its own geometry) ---
  * interpolate_intensities (analysis.py:350-363) -> _interpolate_RBF (analysis.py:249-260)
  * for every pixel: nodes x_n = (lu[p][n], lv[p][n]) and values I[p][n], PIXEL-major as
- * compute_intensities returns them; A_ij = ‖x_i − x_j‖, A w = I solved in fp64 by LU with
- * partial pivoting, f(q_e) = Σ_n w_n ‖q_e − x_n‖ evaluated in fp64 at luv[E][2] (device).
+ * compute_intensities returns them; A_ij = ‖x_i − x_j‖, A w = I solved to fp64 accuracy (what
+ * SciPy's LU with partial pivoting returns, to rounding: fp64 Gauss-Jordan for N <= 80, an fp32
+ * Gauss-Jordan inverse + fp64 iterative refinement above), f(q_e) = Σ_n w_n ‖q_e − x_n‖
+ * evaluated in fp64 at luv[E][2] (device).
  * out: F64 / F32 / I32 / U8, layout RTI_OUT_PIXEL_MAJOR ([p][e], the reference's
  * [y][x][ly][lx]) or RTI_OUT_EVAL_MAJOR ([e][p], prepare_images_data's [ly][lx][y][x]).
  * status: device int the caller zeroes; set to RTI_ERR_SINGULAR when a pixel's system is
