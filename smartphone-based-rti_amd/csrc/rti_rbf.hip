@@ -134,9 +134,10 @@ __device__ __forceinline__ double block_reduce(double v, double* red) {  // ever
 }
 
 template <int NB, typename T>
-__global__ void __launch_bounds__(NB * NB, 4)
+__global__ void __launch_bounds__(NB * NB, NB <= 16 ? 2 : 4)
 rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
-              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status, int max_refine) {
+              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status, int* __restrict__ redo,
+              int max_refine) {
   constexpr int THREADS = NB * NB, WAVES = THREADS / 64, NV = 8 * NB;
   __shared__ double xs[NV], ys[NV], bv[NV], uv[NV], wv[NV], vv[NV], cv[NV], zv[NV], z2v[NV], mv[NV];
   __shared__ __attribute__((aligned(16))) float prow[2][NV], pcol[2][NV];
@@ -218,9 +219,11 @@ rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const 
 
   // Step k = 8·kb + KR: KR is a compile-time constant (the step loop is unrolled by 8), so the pivot
   // row and column are fixed registers of the owning threads.
-  auto step = [&](auto KRc, int kb) __attribute__((always_inline)) -> bool {
+  bool lost = false;  // a non-positive pivot: cond(S) beyond fp32 (the pixel goes to rbf_solve_fp64)
+  auto step = [&](auto KRc, int kb) __attribute__((always_inline)) {
     constexpr int KR = decltype(KRc)::value;
     const int k = 8 * kb + KR, buf = KR & 1;
+    if (k >= n) return;  // uniform
     if (bi == kb) {  // publish row k (this thread's 8 columns of it)
       *reinterpret_cast<float4*>(&prow[buf][j0]) = make_float4(a[KR][0], a[KR][1], a[KR][2], a[KR][3]);
       *reinterpret_cast<float4*>(&prow[buf][j0 + 4]) = make_float4(a[KR][4], a[KR][5], a[KR][6], a[KR][7]);
@@ -231,9 +234,10 @@ rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const 
     }
     __syncthreads();
     const float piv = pcol[buf][k];
-    if (!(piv > 0.f)) return false;  // block-uniform (one LDS word after the barrier)
+    const bool bad = !(piv > 0.f);  // block-uniform (one LDS word after the barrier)
+    lost |= bad;  // no early exit: a straight-line step keeps the block in registers
     const float inv = __builtin_amdgcn_rcpf(piv);  // an approximate inverse is all the refinement needs
-    if (live) {
+    if (live && !bad) {
       const float4 r0 = *reinterpret_cast<const float4*>(&prow[buf][j0]);
       const float4 r1 = *reinterpret_cast<const float4*>(&prow[buf][j0 + 4]);
       const float4 c0 = *reinterpret_cast<const float4*>(&pcol[buf][i0]);
@@ -255,24 +259,25 @@ rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const 
 #pragma unroll
         for (int c = 0; c < 8; ++c) a[r][c] = fmaf(dm[r], nrf[c], a[r][c]);
     }
-    return true;
   };
   using std::integral_constant;
-  for (int kb = 0; kb < nb && !singular; ++kb) {
+  for (int kb = 0; kb < nb && !singular && !lost; ++kb) {
     // steps past n - 1 are skipped (uniform); the LDS buffers alternate with KR's parity, so two
     // consecutive steps never share one (the barrier of step k orders the reads of step k - 2)
-    singular = !step(integral_constant<int, 0>(), kb);
-    if (!singular && 8 * kb + 1 < n) singular = !step(integral_constant<int, 1>(), kb);
-    if (!singular && 8 * kb + 2 < n) singular = !step(integral_constant<int, 2>(), kb);
-    if (!singular && 8 * kb + 3 < n) singular = !step(integral_constant<int, 3>(), kb);
-    if (!singular && 8 * kb + 4 < n) singular = !step(integral_constant<int, 4>(), kb);
-    if (!singular && 8 * kb + 5 < n) singular = !step(integral_constant<int, 5>(), kb);
-    if (!singular && 8 * kb + 6 < n) singular = !step(integral_constant<int, 6>(), kb);
-    if (!singular && 8 * kb + 7 < n) singular = !step(integral_constant<int, 7>(), kb);
+    step(integral_constant<int, 0>(), kb);
+    step(integral_constant<int, 1>(), kb);
+    step(integral_constant<int, 2>(), kb);
+    step(integral_constant<int, 3>(), kb);
+    step(integral_constant<int, 4>(), kb);
+    step(integral_constant<int, 5>(), kb);
+    step(integral_constant<int, 6>(), kb);
+    step(integral_constant<int, 7>(), kb);
   }
 
   double w_t = 0.0;
-  if (!singular) {
+  bool conv = max_refine == 0;  // the refinement reached the fp64 floor (measurement runs without it)
+  bool slow = false;
+  if (!singular && !lost) {
     // dst[i0 + r] = (S⁻¹·x)[i0 + r] for x in LDS; entries of S⁻¹ past n are zero
     auto sinv_times = [&](const double* x, double* dst) __attribute__((always_inline)) {
       double out[8];
@@ -342,12 +347,20 @@ rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const 
       // remaining error ≈ ρ·dn with ρ = dn / dprev the observed contraction (rbf_solve_lds's rule)
       const bool more =
           dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
+      // converged: the last correction is at most 1e-10 of the weights (≈1e-16 at cond 1e4–1e5) and no
+      // sweep above the fp64 floor contracted by less than 4× (error ≈ dn·ρ/(1 − ρ): at ρ → 1 small
+      // corrections hide large errors).  An fp32 inverse of cond ≳ 1e7 contracts slowly, stalls or
+      // diverges instead, and such pixels are solved again in fp64.
+      if (dprev != __builtin_inf() && dn > 1e-14 * wn && dn > 0.25 * dprev) slow = true;
       dprev = dn;
+      conv = dn <= 1e-10 * wn && !slow;
       if (!more && it >= 2 && max_refine >= 0) break;  // uniform: every thread computed the same reductions
     }
   }
   if (singular && t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
-  if (t < N) wT[(int64_t)t * P + p] = singular ? __builtin_nan("") : w_t;
+  const bool again = !singular && (lost || !conv);  // block-uniform
+  if (again && t == 0) redo[p] = 1;
+  if (t < N) wT[(int64_t)t * P + p] = (singular || again) ? __builtin_nan("") : w_t;
 }
 
 // Lower-triangle form (the kernel below): the in-place Gauss-Jordan sweep keeps the matrix symmetric up to
@@ -375,7 +388,8 @@ struct GjsShape {
 template <int NB, typename T>
 __global__ void __launch_bounds__(GjsShape<NB>::THREADS, GjsShape<NB>::MIN_WAVES)
 rbf_solve_gjs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
-              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status, int max_refine) {
+              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status, int* __restrict__ redo,
+              int max_refine) {
   using SH = GjsShape<NB>;
   constexpr int THREADS = SH::THREADS, WAVES = SH::WAVES, NV = SH::NV;
   __shared__ double xs[NV], ys[NV], bv[NV], uv[NV], wv[NV], vv[NV], cv[NV], zv[NV], z2v[NV], mv[NV];
@@ -484,6 +498,7 @@ rbf_solve_gjs(const float* __restrict__ lu, const float* __restrict__ lv, const 
   // Step k = 8·kb + KR (KR compile-time: the loop is unrolled by 8, so the pivot row/column is a fixed
   // register set of its owners).  vcol alternates with KR's parity; the barrier of step k orders the
   // reads of step k − 2.
+  bool lost = false;  // a non-positive pivot: cond(S) beyond fp32 (the pixel goes to rbf_solve_fp64)
   auto step = [&](auto KRc, int kb) __attribute__((always_inline)) {
     constexpr int KR = decltype(KRc)::value;
     const int k = 8 * kb + KR;
@@ -500,7 +515,7 @@ rbf_solve_gjs(const float* __restrict__ lu, const float* __restrict__ lv, const 
     __syncthreads();
     const float piv = v[k];
     const bool bad = !(piv > 0.f);  // block-uniform (one LDS word after the barrier)
-    singular |= bad;  // no early exit: a straight-line step keeps the block in registers
+    lost |= bad;  // no early exit: a straight-line step keeps the block in registers
     // an approximate reciprocal is enough: the inverse only has to be a good approximate inverse
     const float inv = __builtin_amdgcn_rcpf(piv);
     if (liveS && !bad) {
@@ -530,7 +545,7 @@ rbf_solve_gjs(const float* __restrict__ lu, const float* __restrict__ lv, const 
     }
   };
   using std::integral_constant;
-  for (int kb = 0; kb < nb && !singular; ++kb) {
+  for (int kb = 0; kb < nb && !singular && !lost; ++kb) {
     step(integral_constant<int, 0>(), kb);
     step(integral_constant<int, 1>(), kb);
     step(integral_constant<int, 2>(), kb);
@@ -542,7 +557,9 @@ rbf_solve_gjs(const float* __restrict__ lu, const float* __restrict__ lv, const 
   }
 
   double w_t = 0.0;
-  if (!singular) {
+  bool conv = max_refine == 0;  // the refinement reached the fp64 floor (measurement runs without it)
+  bool slow = false;
+  if (!singular && !lost) {
     // S⁻¹ (all of 0..n−1 swept: symmetric again); the asm makes each entry opaque so the 64 fp64
     // conversions are not hoisted out of the refinement loop (128 live registers would spill S⁻¹)
     auto s_elem = [&](int r, int c) __attribute__((always_inline)) {
@@ -587,12 +604,20 @@ rbf_solve_gjs(const float* __restrict__ lu, const float* __restrict__ lv, const 
       // remaining error ≈ ρ·dn with ρ = dn / dprev the observed contraction; at least 3 sweeps
       const bool more =
           dn > 1e-16 * wn && dn < 0.5 * dprev && (dprev == __builtin_inf() || (dn / dprev) * dn > 4e-13 * wn);
+      // converged: the last correction is at most 1e-10 of the weights (≈1e-16 at cond 1e4–1e5) and no
+      // sweep above the fp64 floor contracted by less than 4× (error ≈ dn·ρ/(1 − ρ): at ρ → 1 small
+      // corrections hide large errors).  An fp32 inverse of cond ≳ 1e7 contracts slowly, stalls or
+      // diverges instead, and such pixels are solved again in fp64.
+      if (dprev != __builtin_inf() && dn > 1e-14 * wn && dn > 0.25 * dprev) slow = true;
       dprev = dn;
+      conv = dn <= 1e-10 * wn && !slow;
       if (!more && it >= 2 && max_refine >= 0) break;  // uniform: every thread computed the same reductions
     }
   }
   if (singular && t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
-  if (t < N) wT[(int64_t)t * P + p] = singular ? __builtin_nan("") : w_t;
+  const bool again = !singular && (lost || !conv);  // block-uniform
+  if (again && t == 0) redo[p] = 1;
+  if (t < N) wT[(int64_t)t * P + p] = (singular || again) ? __builtin_nan("") : w_t;
 }
 
 // Wave-wide max of a u32 key: DPP within each row of 16 lanes, then the four row maxima
@@ -772,6 +797,91 @@ rbf_eval(const double* __restrict__ wT, const float2* __restrict__ xyT, int N, i
   }
 }
 
+// ---- fp64 fallback for the pixels the fp32 inverse cannot take ------------------------------------
+// rbf_solve_gji / rbf_solve_gjs flag a pixel (redo[p] = 1) when a Gauss-Jordan pivot of S is not
+// positive in fp32 or the refinement does not reach the fp64 floor — cond(A) ≳ 1e8, i.e. nearly
+// repeated light directions, where SciPy's fp64 LU still returns a solution.  This kernel solves
+// exactly those pixels the way SciPy does: fp64 Gauss-Jordan with partial pivoting on [A | b], the
+// matrix in a per-workgroup global workspace (N·(N+1) doubles, L2/MALL-resident), rows never swapped
+// (a used-row mask; the pivot of step k is the largest |a_ik| among unused rows, ties to the lower
+// row), the system left diagonal, w at node k = b_p / a_pk of step k's pivot row p.  A fixed grid of
+// workgroups strides over the pixels; a pixel without its flag costs one flag load.
+constexpr int RBF_FB_THREADS = 256;
+constexpr int RBF_FB_GRID = 256;
+
+template <typename T>
+__global__ void __launch_bounds__(RBF_FB_THREADS)
+rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
+               const int* __restrict__ redo, double* __restrict__ ws, double* __restrict__ wT,
+               int* __restrict__ status) {
+  __shared__ double xs[RBF_MAX_N], ys[RBF_MAX_N], lf[RBF_MAX_N];
+  __shared__ int used[RBF_MAX_N];
+  __shared__ double s_val[RBF_FB_THREADS / 64];
+  __shared__ int s_row[RBF_FB_THREADS / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int ld = N + 1;
+  double* M = ws + (int64_t)blockIdx.x * N * ld;  // [N][N + 1]: A | b
+  for (int64_t p = blockIdx.x; p < P; p += gridDim.x) {
+    if (!redo[p]) continue;  // block-uniform
+    const int64_t base = p * N;
+    for (int j = t; j < N; j += RBF_FB_THREADS) xs[j] = (double)lu[base + j], ys[j] = (double)lv[base + j], used[j] = 0;
+    __syncthreads();
+    for (int idx = t; idx < N * ld; idx += RBF_FB_THREADS) {
+      const int i = idx / ld, j = idx - i * ld;
+      M[idx] = j < N ? dist64(xs[i], ys[i], xs[j], ys[j]) : ldd(I + base + i);
+    }
+    __syncthreads();
+    bool singular = false;
+    for (int k = 0; k < N; ++k) {
+      // pivot: the largest |a_ik| over unused rows (lower row on ties)
+      double best = -1.0;
+      int row = N;
+      for (int i = t; i < N; i += RBF_FB_THREADS)
+        if (!used[i]) {
+          const double v = fabs(M[(int64_t)i * ld + k]);
+          if (v > best) best = v, row = i;
+        }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const double ob = __shfl_xor(best, off);
+        const int orow = __shfl_xor(row, off);
+        if (ob > best || (ob == best && orow < row)) best = ob, row = orow;
+      }
+      if (lane == 0) s_val[wave] = best, s_row[wave] = row;
+      __syncthreads();
+      best = s_val[0], row = s_row[0];
+#pragma unroll
+      for (int w = 1; w < RBF_FB_THREADS / 64; ++w)
+        if (s_val[w] > best || (s_val[w] == best && s_row[w] < row)) best = s_val[w], row = s_row[w];
+      if (!(best > 0.0)) {  // an exactly zero pivot column: singular (block-uniform)
+        singular = true;
+        break;
+      }
+      const double piv = M[(int64_t)row * ld + k];
+      for (int i = t; i < N; i += RBF_FB_THREADS) lf[i] = i == row ? 0.0 : M[(int64_t)i * ld + k] / piv;
+      __syncthreads();
+      // eliminate column k from every other row (Gauss-Jordan): columns k+1 .. N across the threads
+      const double* prow = M + (int64_t)row * ld;
+      for (int j = k + 1 + t; j <= N; j += RBF_FB_THREADS) {
+        const double pj = prow[j];
+        for (int i = 0; i < N; ++i) M[(int64_t)i * ld + j] = fma(-lf[i], pj, M[(int64_t)i * ld + j]);
+      }
+      if (t == 0) used[row] = k + 1;  // step of this pivot row, + 1
+      __syncthreads();
+    }
+    if (singular) {
+      if (t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
+      for (int j = t; j < N; j += RBF_FB_THREADS) wT[(int64_t)j * P + p] = __builtin_nan("");
+    } else {
+      for (int i = t; i < N; i += RBF_FB_THREADS) {  // row i pivoted step k = used[i] − 1: w_k = b_i / a_ik
+        const int k = used[i] - 1;
+        wT[(int64_t)k * P + p] = M[(int64_t)i * ld + N] / M[(int64_t)i * ld + k];
+      }
+    }
+    __syncthreads();  // xs / used / M are reused by the next flagged pixel
+  }
+}
+
 // fp64 register Gauss-Jordan up to here, rbf_solve_gji above (solve of a 400×400 ROI, MI355X:
 // N = 64: 6.3 vs 13.2 ms, N = 96: 27.9 vs 18.1 ms; tools/time_rbf_solve.py)
 constexpr int RBF_GJ_MAX_N = 80;
@@ -792,20 +902,27 @@ int gji_refine() {
   return v;
 }
 
+bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); }
+
+// redo / fb_ws: the flag per pixel (zeroed) and the fp64 fallback's workspace, when uses_gji(N)
 template <typename T>
 void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
-                  int* status, hipStream_t s) {
+                  int* status, int* redo, double* fb_ws, hipStream_t s) {
   const T* In = static_cast<const T*>(I);
   const dim3 g((unsigned)P);
-  if (N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n())) {
+  if (uses_gji(N)) {
     if (N <= 128)
-      hipLaunchKernelGGL((rbf_solve_gji<16, T>), g, dim3(256), 0, s, lu, lv, In, N, P, wT, xyT, status, gji_refine());
+      hipLaunchKernelGGL((rbf_solve_gji<16, T>), g, dim3(256), 0, s, lu, lv, In, N, P, wT, xyT, status, redo,
+                         gji_refine());
     else if (N <= GjsShape<32>::MAX_N)
       hipLaunchKernelGGL((rbf_solve_gjs<32, T>), g, dim3(GjsShape<32>::THREADS), 0, s, lu, lv, In, N, P, wT, xyT,
-                         status, gji_refine());
+                         status, redo, gji_refine());
     else
-      hipLaunchKernelGGL((rbf_solve_gji<32, T>), g, dim3(1024), 0, s, lu, lv, In, N, P, wT, xyT, status,
+      hipLaunchKernelGGL((rbf_solve_gji<32, T>), g, dim3(1024), 0, s, lu, lv, In, N, P, wT, xyT, status, redo,
                          gji_refine());
+    const unsigned fg = (unsigned)(P < RBF_FB_GRID ? P : RBF_FB_GRID);
+    hipLaunchKernelGGL((rbf_solve_fp64<T>), dim3(fg), dim3(RBF_FB_THREADS), 0, s, lu, lv, In, N, P, redo, fb_ws, wT,
+                       status);
     return;
   }
 #define RBF_GJ(NM)                                                                                       \
@@ -855,15 +972,25 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
   hipStream_t s = (hipStream_t)stream;
   // workspace: per-pixel weights and nodes, node-major ([N][P]) for the coalesced evaluation
   void* ws = nullptr;
-  if (hipMallocAsync(&ws, (size_t)N * P * (sizeof(double) + sizeof(float2)), s) != hipSuccess)
-    return fail(RTI_ERR_HIP, "rti_rbf_perpixel: workspace allocation of %zu bytes failed",
-                (size_t)N * P * (sizeof(double) + sizeof(float2)));
+  // + for the block solvers: a redo flag per pixel and the fp64 fallback's per-workgroup matrices
+  const bool fb = uses_gji(N);
+  const size_t fb_ws_bytes = fb ? (size_t)RBF_FB_GRID * N * (N + 1) * sizeof(double) : 0;
+  const size_t flag_bytes = fb ? ((size_t)P * sizeof(int) + 255) / 256 * 256 : 0;
+  const size_t bytes = (size_t)N * P * (sizeof(double) + sizeof(float2)) + fb_ws_bytes + flag_bytes;
+  if (hipMallocAsync(&ws, bytes, s) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_rbf_perpixel: workspace allocation of %zu bytes failed", bytes);
   double* wT = static_cast<double*>(ws);
   float2* xyT = reinterpret_cast<float2*>(wT + (size_t)N * P);
+  double* fb_ws = reinterpret_cast<double*>(xyT + (size_t)N * P);
+  int* redo = reinterpret_cast<int*>(reinterpret_cast<char*>(fb_ws) + fb_ws_bytes);
+  if (fb && hipMemsetAsync(redo, 0, (size_t)P * sizeof(int), s) != hipSuccess) {
+    (void)hipFreeAsync(ws, s);
+    return fail(RTI_ERR_HIP, "rti_rbf_perpixel: clearing the redo flags failed");
+  }
   switch (in_dtype) {
-    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, s); break;
-    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, s); break;
-    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, s); break;
+    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, s); break;
+    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, s); break;
+    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, s); break;
   }
   switch (out_dtype) {
     case RTI_F64: launch_eval<double>(out_layout, wT, xyT, N, P, luv, E, out, s); break;

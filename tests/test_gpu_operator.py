@@ -200,3 +200,25 @@ def test_rbf_perpixel_large_n_repeated_node_raises(cuda, n):
     with pytest.raises(NotImplementedError):
         rti.interpolate_rbf_perpixel(torch.zeros((1, 257), dtype=torch.int32, device=cuda),
                                      np.zeros((1, 257), np.float32), np.zeros((1, 257), np.float32), qu, qv)
+
+
+@pytest.mark.parametrize("n", [100, 200, 256])
+@pytest.mark.parametrize("d", [1e-5, 1e-6, 1e-7])
+def test_rbf_perpixel_near_repeated_nodes_fp64_fallback(cuda, n, d):
+    """Nearly repeated light directions (cond(A) ~ 1e7 .. 2e9): SciPy's fp64 LU still solves them, the
+    fp32 Gauss-Jordan inverse cannot (non-positive pivot, or a refinement that contracts too slowly).
+    Such pixels are flagged and solved again by the fp64 partial-pivoting fallback; the other pixels
+    of the same launch keep the fast path.  Parity with the oracle at 1e-7 of max(|f|, 255) (both
+    solvers are fp64 with errors ~ cond * eps)."""
+    ys, xs = np.mgrid[0:2, 0:2]
+    rng = np.random.default_rng(n)
+    cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
+    lu, lv = o.light_dirs_for_pixels(cams, xs.ravel(), ys.ravel())
+    lu[2, 7], lv[2, 7] = np.float32(lu[2, 3] + d), lv[2, 3]
+    inten = rng.integers(0, 256, (4, n)).astype(np.int32)
+    qu, qv = rng.uniform(-1, 1, 200), rng.uniform(-1, 1, 200)
+    out = rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv).cpu().numpy()
+    for p in range(4):
+        ref = o.rbf_linear(lu[p], lv[p], inten[p], qu, qv)
+        err, ok = relight_close(out[p], ref, rtol=1e-7 if p == 2 else 1e-8)
+        assert ok, (p, err)
