@@ -805,7 +805,8 @@ rbf_eval(const double* __restrict__ wT, const float2* __restrict__ xyT, int N, i
 // matrix in a per-workgroup global workspace (N·(N+1) doubles, L2/MALL-resident), rows never swapped
 // (a used-row mask; the pivot of step k is the largest |a_ik| among unused rows, ties to the lower
 // row), the system left diagonal, w at node k = b_p / a_pk of step k's pivot row p.  A fixed grid of
-// workgroups strides over the pixels; a pixel without its flag costs one flag load.
+// workgroups strides over the pixels 256 at a time (one flag load per thread, the flagged pixels
+// listed in LDS), so a launch without flagged pixels costs one coalesced pass over the flags.
 constexpr int RBF_FB_THREADS = 256;
 constexpr int RBF_FB_GRID = 256;
 
@@ -819,10 +820,19 @@ rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const
   __shared__ double s_val[RBF_FB_THREADS / 64];
   __shared__ int s_row[RBF_FB_THREADS / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  __shared__ int64_t s_list[RBF_FB_THREADS];
+  __shared__ int s_count;
   const int ld = N + 1;
   double* M = ws + (int64_t)blockIdx.x * N * ld;  // [N][N + 1]: A | b
-  for (int64_t p = blockIdx.x; p < P; p += gridDim.x) {
-    if (!redo[p]) continue;  // block-uniform
+  // the flags of 256 pixels per pass are read in parallel and the flagged ones listed in LDS
+  for (int64_t first = (int64_t)blockIdx.x * RBF_FB_THREADS; first < P; first += (int64_t)gridDim.x * RBF_FB_THREADS) {
+  if (t == 0) s_count = 0;
+  __syncthreads();
+  if (first + t < P && redo[first + t]) s_list[atomicAdd(&s_count, 1)] = first + t;
+  __syncthreads();
+  const int count = s_count;
+  for (int li = 0; li < count; ++li) {
+    const int64_t p = s_list[li];
     const int64_t base = p * N;
     for (int j = t; j < N; j += RBF_FB_THREADS) xs[j] = (double)lu[base + j], ys[j] = (double)lv[base + j], used[j] = 0;
     __syncthreads();
@@ -879,6 +889,8 @@ rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const
       }
     }
     __syncthreads();  // xs / used / M are reused by the next flagged pixel
+  }
+  __syncthreads();  // s_list / s_count are reused by the next pass
   }
 }
 
