@@ -36,13 +36,13 @@ __device__ __forceinline__ double dist64(double xi, double yi, double xj, double
   return sqrt(dx * dx + dy * dy);
 }
 
-// ‖·‖ for the evaluation sweep: fp32 rsqrt seed (≤ 2 ulp, 2⁻²² relative) and one fp64
-// Newton step, d = s·r + (s − (s·r)²)·r/2, relative error ≲ 2⁻⁴⁴ (≈ 6e-14) — 9 issue slots
-// against ≈ 17 for the correctly rounded fp64 sqrt.  With |Σ w_j d_j| terms ≲ 1e5 the
-// interpolated value moves by ≲ 1e-8 absolute.  The solve itself (A and the refinement
-// residuals) keeps the correctly rounded sqrt.
+// ‖·‖ for the evaluation sweep: the fp64 rsq approximation and one Newton step,
+// d = s·r + (s − (s·r)²)·r/2 — 8 issue slots against ≈ 17 for the correctly rounded fp64 sqrt.
+// (The fp32 rsq seed with conversions and a clamp ran at the same speed on MI355X, 229.6 vs 230.4 ms
+// for N = 200, with 4× the error against SciPy: 1.8e-11 vs 4.3e-12 of max(|f|, 255).)  The solve
+// itself (A and the refinement residuals) keeps the correctly rounded sqrt.
 __device__ __forceinline__ double norm_eval(double s) {
-  const double r = (double)__builtin_amdgcn_rsqf(fmaxf((float)s, 1e-30f));
+  const double r = __builtin_amdgcn_rsq(fmax(s, 1e-300));
   const double d0 = s * r;
   return fma(fma(-d0, d0, s), 0.5 * r, d0);
 }
