@@ -222,3 +222,34 @@ def test_rbf_perpixel_near_repeated_nodes_fp64_fallback(cuda, n, d):
         ref = o.rbf_linear(lu[p], lv[p], inten[p], qu, qv)
         err, ok = relight_close(out[p], ref, rtol=1e-7 if p == 2 else 1e-8)
         assert ok, (p, err)
+
+
+def test_rbf_perpixel_query_on_a_node(cuda):
+    """A grid query that coincides exactly with a light direction (distance 0 in the evaluation sweep)
+    gives the node's own value: finite, and equal to the oracle's (the sweep biases ‖q − x‖² by 1e-300
+    instead of clamping every term)."""
+    ys, xs = np.mgrid[0:2, 0:2]
+    n = 40
+    rng = np.random.default_rng(5)
+    cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
+    lu, lv = o.light_dirs_for_pixels(cams, xs.ravel(), ys.ravel())
+    lu[:, 5], lv[:, 5] = np.float32(0.5), np.float32(-0.5)  # exactly on the reference's 0.02 grid
+    inten = rng.integers(0, 256, (4, n)).astype(np.int32)
+    xf = np.around(np.arange(-1, 1, 0.02), 2)
+    qu, qv = np.tile(xf, 100), np.repeat(xf, 100)
+    for m in (n, 100, 200):  # fp64 register GJ, and the block solvers
+        if m != n:
+            extra = o.light_dirs_for_pixels(np.stack([rng.uniform(-100, 100, m - n), rng.uniform(-100, 100, m - n),
+                                                      rng.uniform(60, 150, m - n)], -1), xs.ravel(), ys.ravel())
+            lum, lvm = np.concatenate([lu, extra[0]], 1), np.concatenate([lv, extra[1]], 1)
+            im = np.concatenate([inten, rng.integers(0, 256, (4, m - n)).astype(np.int32)], 1)
+        else:
+            lum, lvm, im = lu, lv, inten
+        out = rti.interpolate_rbf_perpixel(torch.as_tensor(im, device=cuda), lum, lvm, qu, qv).cpu().numpy()
+        assert np.isfinite(out).all()
+        on = np.flatnonzero((qu == 0.5) & (qv == -0.5))
+        for p in range(4):
+            ref = o.rbf_linear(lum[p], lvm[p], im[p], qu, qv)
+            err, ok = relight_close(out[p], ref, rtol=1e-8)
+            assert ok, (m, p, err)
+            assert abs(out[p][on[0]] - im[p][5]) < 1e-6
