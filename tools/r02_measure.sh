@@ -16,10 +16,10 @@ run() {  # name seconds cmd...
   case $rc in 124|134|137|139) echo "fatal rc=$rc"; exit $rc;; esac
   return 0
 }
-for c in ${CONFIGS:-c3 c2 c4 c10 c5 c9 c6 c7 c8}; do
-  budget=8; [ $c = c3 ] && budget=16
+for c in ${CONFIGS:-c3 c2 c4 c10 c5 c9 c6 c7 c8 c8n200}; do
+  budget=8; [ $c = c3 ] && budget=16; extra=""; [ $c = c8n200 ] && extra="--no-cpu"
   run bench_$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_$c -o run -- \
-      python3 bench.py --config $c --cpu-budget $budget
+      python3 bench.py --config $c --cpu-budget $budget $extra
 done
 if [ -z "$SKIP_EXTRA" ]; then
   run bench_c5_hot 200 python3 bench.py --config c5 --map-sets 1 --no-cpu
