@@ -32,6 +32,7 @@ def main():
                     "valu:planar:nt,valu:planar:nt+nts,valu:planar:nt+lds+nts,valu:planar:nt+lds,"
                     "mfma:planar:nt,mfma:pixel:nt")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--store-windows", default="", help="PTM-6 store probe wrapping its stores inside W MiB (list)")
     ap.add_argument("--rows", type=int, default=0, help="override the config's H (row-shard sizes: 2160/G)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -85,6 +86,8 @@ def main():
                 variants.append((f"probe_fit6_{nm}", "pfit", str(pvnt), 0))
             for pvnt, nm in ((0, "plain"), (4, "win64K")):
                 variants.append((f"probe_store_{nm}", "pstore", str(pvnt), 0))
+            for mib in filter(None, args.store_windows.split(",")):
+                variants.append((f"probe_store_win{mib}M", "pstore", str(100 + int(mib)), 0))
             probe.probe_persist.argtypes = probe.probe_fit6.argtypes
             for v in (1256, 1512, 2256, 2512, 3256, 1768, 2384):
                 variants.append((f"probe_persist_F{v // 1000}_wg{v % 1000}", "ppersist", str(v), 0))
