@@ -749,12 +749,12 @@ rbf_solve_gj(const float* __restrict__ lu, const float* __restrict__ lv, const T
 template <int TE, typename TO, int OL>
 __global__ void __launch_bounds__(256)
 rbf_eval(const double* __restrict__ wT, const float2* __restrict__ xyT, int N, int64_t P,
-         const double* __restrict__ luv, int E, TO* __restrict__ out) {
+         const double* __restrict__ luv, int E, TO* __restrict__ out, int64_t pbase) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int e0 = (blockIdx.x * 4 + wave) * TE;
   if (e0 >= E) return;  // wave-uniform
-  const int64_t p = (int64_t)blockIdx.y * 64 + lane;
+  const int64_t p = pbase + (int64_t)blockIdx.y * 64 + lane;
   const int64_t pc = p < P ? p : P - 1;
   double qu[TE], qv[TE], acc[TE];
 #pragma unroll
@@ -951,16 +951,23 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
 #undef RBF_GJ
 }
 
+// grid x = eval groups, y = 64-pixel tiles (consecutive blocks share a tile's nodes and weights in
+// L2); more than 65535 tiles (P > 4.19 M) go out as several launches over pixel ranges
 template <typename TO>
 void launch_eval(int ol, const double* wT, const float2* xyT, int N, int64_t P, const double* luv, int E, void* out,
                  hipStream_t s) {
-  const dim3 g((unsigned)((E + 4 * RBF_TE - 1) / (4 * RBF_TE)), (unsigned)((P + 63) / 64));
-  if (ol == RTI_OUT_PIXEL_MAJOR)
-    hipLaunchKernelGGL((rbf_eval<RBF_TE, TO, RTI_OUT_PIXEL_MAJOR>), g, dim3(256), 0, s, wT, xyT, N, P, luv, E,
-                       static_cast<TO*>(out));
-  else
-    hipLaunchKernelGGL((rbf_eval<RBF_TE, TO, RTI_OUT_EVAL_MAJOR>), g, dim3(256), 0, s, wT, xyT, N, P, luv, E,
-                       static_cast<TO*>(out));
+  constexpr int64_t TILES = 65535;
+  const unsigned gx = (unsigned)((E + 4 * RBF_TE - 1) / (4 * RBF_TE));
+  for (int64_t pb = 0; pb < P; pb += TILES * 64) {
+    const int64_t tiles = (P - pb + 63) / 64 < TILES ? (P - pb + 63) / 64 : TILES;
+    const dim3 g(gx, (unsigned)tiles);
+    if (ol == RTI_OUT_PIXEL_MAJOR)
+      hipLaunchKernelGGL((rbf_eval<RBF_TE, TO, RTI_OUT_PIXEL_MAJOR>), g, dim3(256), 0, s, wT, xyT, N, P, luv, E,
+                         static_cast<TO*>(out), pb);
+    else
+      hipLaunchKernelGGL((rbf_eval<RBF_TE, TO, RTI_OUT_EVAL_MAJOR>), g, dim3(256), 0, s, wT, xyT, N, P, luv, E,
+                         static_cast<TO*>(out), pb);
+  }
 }
 
 }  // namespace
@@ -982,8 +989,8 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
     return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: out dtype %d", out_dtype);
   if (out_layout != RTI_OUT_PIXEL_MAJOR && out_layout != RTI_OUT_EVAL_MAJOR)
     return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: out layout %d", out_layout);
-  if ((int64_t)((E + 4 * RBF_TE - 1) / (4 * RBF_TE)) > 0x7fffffff || (P + 63) / 64 > 65535)
-    return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: grid too large (P=%lld, E=%d)", (long long)P, E);
+  if ((int64_t)((E + 4 * RBF_TE - 1) / (4 * RBF_TE)) > 0x7fffffff)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: grid too large (E=%d)", E);
   hipStream_t s = (hipStream_t)stream;
   // workspace: per-pixel weights and nodes, node-major ([N][P]) for the coalesced evaluation
   void* ws = nullptr;

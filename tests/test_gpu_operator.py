@@ -253,3 +253,28 @@ def test_rbf_perpixel_query_on_a_node(cuda):
             err, ok = relight_close(out[p], ref, rtol=1e-8)
             assert ok, (m, p, err)
             assert abs(out[p][on[0]] - im[p][5]) < 1e-6
+
+
+def test_rbf_perpixel_large_roi_past_65535_tiles(cuda):
+    """A 2100 x 2100 ROI (4.41 M pixels: more 64-pixel tiles than one launch's grid-y holds) is
+    evaluated in pixel-range launches; pixels on both sides of the 4.19 M boundary match the oracle."""
+    H = W = 2100
+    n = 20
+    rng = np.random.default_rng(21)
+    cams = np.stack([rng.uniform(-600, 2700, n), rng.uniform(-600, 2700, n), rng.uniform(300, 900, n)], -1)
+    lu, lv = rti.light_dirs(cams, H, W, device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    inten = torch.randint(0, 256, (H, W, n), generator=g, device=cuda, dtype=torch.int32)
+    qu, qv = rng.uniform(-1, 1, 12), rng.uniform(-1, 1, 12)
+    out = rti.interpolate_rbf_perpixel(inten, lu, lv, qu, qv)
+    P = H * W
+    idx = np.concatenate([[0, 1, 65535 * 64 - 1, 65535 * 64, 65535 * 64 + 1, P - 1],
+                          rng.integers(0, P, 40)])
+    lu_h = lu.reshape(P, n)[idx].cpu().numpy()
+    lv_h = lv.reshape(P, n)[idx].cpu().numpy()
+    i_h = inten.reshape(P, n)[idx].cpu().numpy()
+    got = out.reshape(P, -1)[idx].cpu().numpy()
+    for k in range(len(idx)):
+        ref = o.rbf_linear(lu_h[k], lv_h[k], i_h[k], qu, qv)
+        err, ok = relight_close(got[k], ref, rtol=1e-8)
+        assert ok, (int(idx[k]), err)
