@@ -1019,15 +1019,18 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
   }
   if (a.nc == 0) {
     // AUTO chunks per lane (PTM-6, 4-byte intensities): the longest per-wave run in each
-    // plane whose accumulators fit, as long as the launch keeps >= 2000 waves (≈2 per SIMD;
-    // c2 is faster at 4 chunks than at 8).  HSH-16 measured no gain (c4: 3.88 ms at 1 and 2
-    // chunks, 4.57 at 3) and keeps one chunk, as do the LDS-weight tuning variants.
+    // plane whose accumulators fit, as long as the launch keeps >= 1000 waves (≈1 per SIMD).
+    // r02 sweeps (profiles/r02_chunks_c2_shards_sweep.log, interleaved): c2 8 chunks (1012
+    // waves) 0.0712 vs 4 chunks 0.0734 ms; 540-row shard 8: 0.1294 vs 4: 0.1335 ms; 270-row
+    // shard 4 (1012 waves) 0.0675 vs 2 0.0679 vs 8 (506 waves) 0.0950 ms.  HSH-16 measured no
+    // gain (c4: 3.88 ms at 1 and 2 chunks, 4.57 at 3) and keeps one chunk, as do the
+    // LDS-weight tuning variants.
     const bool plain = (a.mode & ~(VM_NT | VM_NTS | VM_STAGE)) == 0;
     a.nc = 1;
     if (plain && in_dtype != RTI_U8 && k == 6) {
       const int64_t groups = P * C / 4;  // 4-pixel lane groups
       for (int nc = 8; nc > 1; nc >>= 1)
-        if (groups / (64 * nc) >= 2000) {
+        if (groups / (64 * nc) >= 1000) {
           a.nc = nc;
           break;
         }
