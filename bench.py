@@ -1026,7 +1026,7 @@ def main():
                                 "mean": round(float(wms.mean()), 5), "n": 50, "launches_per_window": m,
                                 "warmup": 10, "per_launch_median": round(float(np.median(kms)), 5),
                                 "per_launch_min": round(float(kms.min()), 5),
-                                "per_launch_mean": round(float(kms.mean()), 5), "n": int(kms.size), "warmup": 10,
+                                "per_launch_mean": round(float(kms.mean()), 5), "per_launch_n": int(kms.size),
                                 "per_rank_median": [round(x, 5) for x in kernel_ms_rank]},
             "parity": parity,
             "cpu_baseline": cpu,

@@ -29,6 +29,20 @@
 #include "rti_internal.h"
 
 namespace rti {
+
+// compute units of the current device (cached; 256 on MI355X)
+int device_cus() {
+  static int cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -70,7 +84,8 @@ __device__ __forceinline__ void store_f32(float* __restrict__ dst, const float (
 //   VM_STAGE : pixel-major output transposed through LDS so every store instruction
 //              writes 1 KiB contiguous (a lane's own VEC*K floats sit at a 4*VEC*K-byte
 //              lane stride otherwise)
-constexpr int VM_NT = 1, VM_LDS = 2, VM_NTS = 4, VM_STAGE = 8;
+//   VM_ROT   : each wave sweeps the lights from its own start plane (measurement variant)
+constexpr int VM_NT = 1, VM_LDS = 2, VM_NTS = 4, VM_STAGE = 8, VM_ROT = 16;
 
 template <int N, bool NT>
 __device__ __forceinline__ void store_f32_nt(float* __restrict__ dst, const float (&v)[N]) {
@@ -103,7 +118,7 @@ constexpr bool stage_ok() { return VEC == 4 && (VEC * K) % 4 == 0 && K <= 9; }
 // dynamic LDS: [pinv weights N*KP floats, 16-B aligned][staging 4 waves * 64 lanes * VEC*K floats]
 template <int K, int VEC, int NC, typename T, int LAYOUT, int MODE, bool TAIL>
 __device__ __forceinline__ void fit_valu_body(const float* __restrict__ pinv, int N, const T* __restrict__ I,
-                                              int64_t P, int64_t lstride, float* __restrict__ dst, int64_t pbase,
+                                              int64_t P, int64_t pe, int64_t lstride, float* __restrict__ dst, int64_t pbase,
                                               int64_t wave_base, const float* lds_w, float* lds_dyn) {
   constexpr bool NT = (MODE & VM_NT) != 0;
   constexpr bool LDSW = (MODE & VM_LDS) != 0;
@@ -118,7 +133,7 @@ __device__ __forceinline__ void fit_valu_body(const float* __restrict__ pinv, in
   int coff[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    ok[c] = !TAIL || pbase + (int64_t)c * CH < P;
+    ok[c] = !TAIL || pbase + (int64_t)c * CH < pe;
     coff[c] = ok[c] ? c * CH : 0;
   }
 
@@ -137,36 +152,47 @@ __device__ __forceinline__ void fit_valu_body(const float* __restrict__ pinv, in
 
   constexpr int U = (VEC >= 16) ? 4 : 8;            // loads in flight per lane
   constexpr int UP = U / NC > 0 ? U / NC : 1;        // light planes per step
-  int n = 0;
-  for (; n + UP <= N; n += UP) {
-    float x[UP][NC][VEC];
+  // lights [nb, ne) of the sweep; VM_ROT (measurement variant) starts each wave at its own light
+  // r0 and wraps, so the waves in flight read different planes at any moment
+  auto sweep = [&](int nb, int ne) {
+    int n = nb;
+    for (; n + UP <= ne; n += UP) {
+      float x[UP][NC][VEC];
 #pragma unroll
-    for (int u = 0; u < UP; ++u)
+      for (int u = 0; u < UP; ++u)
 #pragma unroll
-      for (int c = 0; c < NC; ++c) load_px<T, VEC, NT>(src + (int64_t)(n + u) * lstride + coff[c], x[u][c]);
+        for (int c = 0; c < NC; ++c) load_px<T, VEC, NT>(src + (int64_t)(n + u) * lstride + coff[c], x[u][c]);
 #pragma unroll
-    for (int u = 0; u < UP; ++u)
+      for (int u = 0; u < UP; ++u)
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float w = weight(k, n + u);
+        for (int k = 0; k < K; ++k) {
+          const float w = weight(k, n + u);
 #pragma unroll
-        for (int c = 0; c < NC; ++c)
+          for (int c = 0; c < NC; ++c)
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) acc[k][c * VEC + v] = fmaf(w, x[u][c][v], acc[k][c * VEC + v]);
-      }
-  }
-  for (; n < N; ++n) {
+            for (int v = 0; v < VEC; ++v) acc[k][c * VEC + v] = fmaf(w, x[u][c][v], acc[k][c * VEC + v]);
+        }
+    }
+    for (; n < ne; ++n) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      float x[VEC];
-      load_px<T, VEC, NT>(src + (int64_t)n * lstride + coff[c], x);
+      for (int c = 0; c < NC; ++c) {
+        float x[VEC];
+        load_px<T, VEC, NT>(src + (int64_t)n * lstride + coff[c], x);
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float w = weight(k, n);
+        for (int k = 0; k < K; ++k) {
+          const float w = weight(k, n);
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) acc[k][c * VEC + v] = fmaf(w, x[v], acc[k][c * VEC + v]);
+          for (int v = 0; v < VEC; ++v) acc[k][c * VEC + v] = fmaf(w, x[v], acc[k][c * VEC + v]);
+        }
       }
     }
+  };
+  if constexpr ((MODE & VM_ROT) != 0) {
+    const int r0 = (int)(((wave_base / (64 * VEC * NC)) * 13) % N);
+    sweep(r0, N);
+    sweep(0, r0);
+  } else {
+    sweep(0, N);
   }
 
 #pragma unroll
@@ -191,7 +217,7 @@ __device__ __forceinline__ void fit_valu_body(const float* __restrict__ pinv, in
         constexpr int F = VEC * K;  // floats per lane (24 for PTM-6)
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         const int64_t cbase = wave_base + (int64_t)c * CH;  // the wave's first pixel of chunk c
-        if (cbase + CH <= P) {  // wave-uniform: the whole chunk's 64*F floats are in range
+        if (cbase + CH <= pe) {  // wave-uniform: the whole chunk's 64*F floats are in range
           const int woff = LDSW ? ((N * KP + 3) & ~3) : 0;
           float* st = lds_dyn + woff + wave * 64 * F;
 #pragma unroll
@@ -219,7 +245,7 @@ __device__ __forceinline__ void fit_valu_body(const float* __restrict__ pinv, in
 
 template <int K, int VEC, int NC, typename T, int LAYOUT, int MODE>
 __global__ void __launch_bounds__(256)
-fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P,
+fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t pb, int64_t pe,
                 int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
   constexpr bool LDSW = (MODE & VM_LDS) != 0;
   constexpr int KP = (K + 3) & ~3;
@@ -233,15 +259,15 @@ fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, 
     __syncthreads();
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t wave_base = ((int64_t)blockIdx.x * 4 + wave) * (64 * VEC * NC);
+  const int64_t wave_base = pb + ((int64_t)blockIdx.x * 4 + wave) * (64 * VEC * NC);  // pixels [pb, pe) of P
   const int64_t pbase = wave_base + (int64_t)lane * VEC;
-  if (pbase >= P) return;
+  if (pbase >= pe) return;
   const T* __restrict__ Ic = I + (int64_t)blockIdx.y * cstride;
   float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
-  if (NC == 1 || wave_base + (int64_t)(64 * VEC * NC) <= P)  // wave-uniform
-    fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, false>(pinv, N, Ic, P, lstride, dst, pbase, wave_base, lds_w, lds_dyn);
+  if (NC == 1 || wave_base + (int64_t)(64 * VEC * NC) <= pe)  // wave-uniform
+    fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, false>(pinv, N, Ic, P, pe, lstride, dst, pbase, wave_base, lds_w, lds_dyn);
   else
-    fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, true>(pinv, N, Ic, P, lstride, dst, pbase, wave_base, lds_w, lds_dyn);
+    fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, true>(pinv, N, Ic, P, pe, lstride, dst, pbase, wave_base, lds_w, lds_dyn);
 }
 
 // ---- MFMA kernel (k <= 16) ------------------------------------------------------------
@@ -438,8 +464,8 @@ fit_shared_tile(const float* __restrict__ pinv, int k, int N, const T* __restric
 // plane at RC = 16), the next step's loads in registers during the compute, two barriers per step.
 template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT, bool STORE = true>
 __global__ void __launch_bounds__(64 * W)
-fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P,
-                  int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P, int64_t pb,
+                  int64_t pe, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
   constexpr int R = 256 * RC, S = W, G = R / (64 * W);  // G = 64-pixel groups per wave
   static_assert(G >= 1 && R % (64 * W) == 0, "tile must split into 64-pixel groups per wave");
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
@@ -451,11 +477,11 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
     lds_pinv[idx] = (i < k && n < N) ? pinv[i * N + n] : 0.f;
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t t0 = (int64_t)blockIdx.x * R;
+  const int64_t t0 = pb + (int64_t)blockIdx.x * R;  // pixels [pb, pe) of P
   const T* __restrict__ src = I + (int64_t)blockIdx.y * cstride + t0 + 4 * lane;
   bool pin[RC];
 #pragma unroll
-  for (int c = 0; c < RC; ++c) pin[c] = t0 + 256 * c + 4 * lane < P;
+  for (int c = 0; c < RC; ++c) pin[c] = t0 + 256 * c + 4 * lane < pe;
   auto load = [&](int t, floatx4 (&st)[RC]) {
     const int n = t * S + wave;
 #pragma unroll
@@ -546,7 +572,7 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int64_t px = t0 + pw + 64 * g + 4 * q;
-    if (px >= P) continue;
+    if (px >= pe) continue;
     if constexpr (LAYOUT == RTI_COEF_PLANAR) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
@@ -705,18 +731,20 @@ struct FitArgs {
   int mode;  // VALU variant bits (VM_*)
   int nc;    // VALU chunks per lane (1 = one VEC-pixel group per lane)
   hipStream_t stream;
+  int64_t pb = 0, pe = 0;  // this launch's pixel range [pb, pe) (pe 0 = P): VALU and 8-wave tile kernels
 };
 
 template <int K, int VEC, int NC, typename T, int LAYOUT, int MODE>
 void launch_valu_t(const FitArgs& a) {
-  const int64_t groups = (a.P + VEC * NC - 1) / (VEC * NC);
+  const int64_t pe = a.pe ? a.pe : a.P;
+  const int64_t groups = (pe - a.pb + VEC * NC - 1) / (VEC * NC);
   dim3 grid(grid_1d(groups, 256), a.C);
   constexpr int KP = (K + 3) & ~3;
   size_t lds = (MODE & VM_LDS) ? (((size_t)a.N * KP + 3) & ~(size_t)3) * sizeof(float) : 0;
   if constexpr ((MODE & VM_STAGE) && LAYOUT == RTI_COEF_PIXEL_MAJOR && stage_ok<K, VEC>())
     lds += (size_t)4 * 64 * VEC * K * sizeof(float);
   hipLaunchKernelGGL((fit_shared_valu<K, VEC, NC, T, LAYOUT, MODE>), grid, dim3(256), lds, a.stream, a.pinv, a.N,
-                     static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride);
+                     static_cast<const T*>(a.I), a.P, a.pb, pe, a.lstride, a.cstride, a.coef, a.ocstride);
 }
 
 // chunks per lane instantiated per k (accumulators K*NC*VEC must fit the 256 VGPRs of a wave)
@@ -726,6 +754,9 @@ constexpr int nc_max() { return K <= 6 ? 8 : (K <= 9 ? 4 : 3); }
 template <int K, int VEC, int NC, typename T, int LAYOUT>
 void launch_valu_ncm(const FitArgs& a) {
   const int m = a.mode & (VM_NT | VM_NTS | VM_STAGE);
+  if constexpr (K == 6 && VEC == 4 && NC >= 4 && std::is_same<T, float>::value && LAYOUT == RTI_COEF_PIXEL_MAJOR) {
+    if (a.mode & VM_ROT) return launch_valu_t<K, VEC, NC, T, LAYOUT, VM_NT | VM_STAGE | VM_ROT>(a);
+  }
   if (m == (VM_NT | VM_NTS)) launch_valu_t<K, VEC, NC, T, LAYOUT, VM_NT | VM_NTS>(a);
   else if (m == (VM_NT | VM_STAGE)) launch_valu_t<K, VEC, NC, T, LAYOUT, VM_NT | VM_STAGE>(a);
   else if (m & VM_NT) launch_valu_t<K, VEC, NC, T, LAYOUT, VM_NT>(a);
@@ -856,9 +887,10 @@ int launch_tile_w_t(const FitArgs& a) {
   if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
-  dim3 grid(grid_1d(a.P, R), a.C);
+  const int64_t pe = a.pe ? a.pe : a.P;
+  dim3 grid(grid_1d(pe - a.pb, R), a.C);
   hipLaunchKernelGGL(kern, grid, dim3(64 * W), lds, a.stream, a.pinv, a.k, a.N, static_cast<const T*>(a.I), a.P,
-                     a.lstride, a.cstride, a.coef, a.ocstride);
+                     a.pb, pe, a.lstride, a.cstride, a.coef, a.ocstride);
   return RTI_OK;
 }
 
@@ -955,6 +987,96 @@ size_t dtype_size(int dt) {
   }
 }
 
+// ---- launch generations (r02) ---------------------------------------------------------------
+// The stack streams fastest when every wave on the chip sweeps the light planes in step with the
+// others, so that at any moment they all read one contiguous slab of the same plane.  The waves of
+// ONE launch start together and, with equal work, stay in step; the waves that start as earlier
+// ones retire (a second "generation" inside the same launch) do not.  Measured on c3 (4K x 100,
+// PTM-6, interleaved, profiles/r02_generations_sweep.log): one launch of 4050 waves 0.562 ms, the
+// same pixels as 2 launches of 2025 waves 0.540, as 4 launches of 1013 waves (one per SIMD)
+// 0.510 ms; launches of 1350 waves (a partial second wave on a third of the SIMDs) 0.637, and each
+// wave starting its sweep at its own plane 0.69 ms.  So a large fit is issued as consecutive
+// launches that give every SIMD one or two waves (VALU stream) or four workgroup rounds (8-wave tile), each
+// over a pixel range [pb, pe) of every plane (same kernels, same per-pixel arithmetic: the
+// coefficients are bit-identical to one launch).
+struct Generations {
+  bool split = false;  // false: one launch over all channels
+  int parts = 1;       // launches per channel when split
+  int64_t unit = 1;    // pixels per wave (VALU) or per workgroup tile; part bounds are multiples of it
+};
+
+// VALU stream (PTM-6 fp32, AUTO): chunks per lane nc and launches such that every launch gives
+// every SIMD the same number of waves, one or two (all resident at once: one generation), trying
+// nc = 4, 8, 2 in that order.  Two boxes agreed on nc = 4 (c3 as 4 launches of 2025 waves: 0.533 and
+// 0.534 ms, against 0.562 / 0.597 for one launch at nc = 8); 8 chunks at one wave per SIMD ran
+// 0.510 ms on one box and 0.575 on the other (profiles/r02_generations_sweep.log).  Parts that would
+// move < 256 MiB stay one launch (a launch boundary costs a few microseconds).  Returns nc (0: no
+// balanced split; the >= 1000-wave rule applies).
+int valu_generations(const FitArgs& a, size_t es, Generations& g) {
+  const int64_t simds = 4 * (int64_t)device_cus();
+  auto balanced = [&](int64_t w) { return (w * 100 >= simds * 85 && w <= simds) || (w * 100 >= simds * 170 && w <= 2 * simds); };
+  for (int nc : {4, 8, 2}) {
+    const int64_t ppw = 256 * nc, wpc = (a.P + ppw - 1) / ppw, total = wpc * a.C;
+    Generations t;
+    t.unit = ppw;
+    int64_t per = total;
+    if (total > 2 * simds) {
+      t.split = true;
+      t.parts = (int)((wpc + 2 * simds - 1) / (2 * simds));
+      per = (wpc + t.parts - 1) / t.parts;
+    }
+    if (!balanced(per)) continue;
+    if (t.split && (double)per * ppw * a.N * es < 256.0 * (1 << 20)) return 0;
+    g = t;
+    return nc;
+  }
+  return 0;
+}
+
+// 8-wave tile kernel (one 4096-pixel workgroup per CU): launches of <= 4 rounds of workgroups per
+// channel, the parts count chosen so the last round is >= 85 % full (c4 4K RGB x 200: 3.74 ms one
+// launch, 3.61 one per channel, 3.57 two per channel = 1013 tiles; 1350-tile launches 3.82 ms).
+Generations tile_generations(const FitArgs& a, int64_t tile_px) {
+  const int64_t cus = device_cus(), cap = 4 * cus;
+  const int64_t tpc = (a.P + tile_px - 1) / tile_px;
+  Generations g;
+  g.unit = tile_px;
+  if (tpc * a.C <= cap) return g;
+  g.split = true;
+  const int p0 = (int)((tpc + cap - 1) / cap);
+  g.parts = p0;
+  for (int p = p0; p < p0 + 4; ++p) {
+    const int64_t per = (tpc + p - 1) / p, last = per % cus;
+    if (last == 0 || last * 100 >= cus * 85) {
+      g.parts = p;
+      break;
+    }
+  }
+  return g;
+}
+
+// run `launch` over the generations: per channel (C = 1 views of I and coef), pixel ranges of
+// whole units
+template <typename F>
+int launch_generations(const FitArgs& a, size_t es, const Generations& g, F&& launch) {
+  if (!g.split) return launch(a);
+  const int64_t units = (a.P + g.unit - 1) / g.unit, per = (units + g.parts - 1) / g.parts;
+  for (int c = 0; c < a.C; ++c) {
+    FitArgs b = a;
+    b.C = 1;
+    b.I = static_cast<const char*>(a.I) + (size_t)c * a.cstride * es;
+    b.coef = a.coef + (size_t)c * a.ocstride;
+    for (int i = 0; i < g.parts; ++i) {
+      b.pb = i * per * g.unit;
+      b.pe = (i + 1) * per * g.unit < a.P ? (i + 1) * per * g.unit : a.P;
+      if (b.pb >= b.pe) break;
+      const int st = launch(b);
+      if (st != RTI_OK) return st;
+    }
+  }
+  return RTI_OK;
+}
+
 }  // namespace
 }  // namespace rti
 
@@ -1015,8 +1137,9 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     // PTM-6 pixel-major coefficients leave through LDS as whole 1 KiB rows per store
     // instruction: with wide lanes the direct 96-B-strided stores raised WRITE_SIZE to 1.46x
     // the coefficient bytes (c3 0.573 -> 0.549 ms, c2 0.082 -> 0.072 ms staged)
-    a.mode = VM_NT | (k == 6 ? VM_STAGE : 0);
+    a.mode = VM_NT | (k == 6 ? VM_STAGE : 0) | ((kernel & RTI_KERNEL_ROTATE) ? VM_ROT : 0);
   }
+  Generations gens;  // one launch unless AUTO splits it (launch generations, above)
   if (a.nc == 0) {
     // AUTO chunks per lane (PTM-6, 4-byte intensities): the longest per-wave run in each
     // plane whose accumulators fit, as long as the launch keeps >= 1000 waves (≈1 per SIMD).
@@ -1025,15 +1148,23 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     // shard 4 (1012 waves) 0.0675 vs 2 0.0679 vs 8 (506 waves) 0.0950 ms.  HSH-16 measured no
     // gain (c4: 3.88 ms at 1 and 2 chunks, 4.57 at 3) and keeps one chunk, as do the
     // LDS-weight tuning variants.
-    const bool plain = (a.mode & ~(VM_NT | VM_NTS | VM_STAGE)) == 0;
+    // r02: fp32 AUTO picks nc and the launch generations together (valu_generations above).
+    const bool plain = (a.mode & ~(VM_NT | VM_NTS | VM_STAGE | VM_ROT)) == 0;
     a.nc = 1;
     if (plain && in_dtype != RTI_U8 && k == 6) {
-      const int64_t groups = P * C / 4;  // 4-pixel lane groups
-      for (int nc = 8; nc > 1; nc >>= 1)
-        if (groups / (64 * nc) >= 1000) {
-          a.nc = nc;
-          break;
-        }
+      int gnc = 0;
+      if (sel == RTI_KERNEL_AUTO && in_dtype == RTI_F32 && !(kernel & RTI_KERNEL_ONE_LAUNCH) && vec_ok_for(4))
+        gnc = valu_generations(a, es, gens);
+      if (gnc) {
+        a.nc = gnc;
+      } else {
+        const int64_t groups = P * C / 4;  // 4-pixel lane groups
+        for (int nc = 8; nc > 1; nc >>= 1)
+          if (groups / (64 * nc) >= 1000) {
+            a.nc = nc;
+            break;
+          }
+      }
     }
   }
   const bool mfma_ok = N <= 1024 && P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 &&
@@ -1052,12 +1183,13 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
       // AUTO (no tile bits set) for fp32 at N <= 512: the 8-wave kernel on ONE 4096-pixel LDS tile
       // (16 KiB per wave and plane; c4 3.74 vs 3.93 ms for the 2048-pixel double-buffered tile,
       // profiles/r02_c4_tile_rc16_sweep.log); above N = 512 its [N][16] pinv no longer fits.
-      const bool tile_auto = (kernel & ~0xff & ~RTI_KERNEL_NONTEMPORAL) == 0 && N <= 512;
+      const bool tile_auto = (kernel & ~0xff & ~(RTI_KERNEL_NONTEMPORAL | RTI_KERNEL_ONE_LAUNCH)) == 0 && N <= 512;
       const int rc0 = rc ? rc : (N <= 512 ? 8 : 4);
       int st;
       switch (in_dtype) {
         case RTI_F32:
-          st = tile_auto ? launch_tile<float>(a, 15, 1, 1, 8)
+          if (tile_auto && !(kernel & RTI_KERNEL_ONE_LAUNCH)) gens = tile_generations(a, 4096);
+          st = tile_auto ? launch_generations(a, es, gens, [](const FitArgs& b) { return launch_tile<float>(b, 15, 1, 1, 8); })
                          : launch_tile<float>(a, rc0, sp ? sp : 2, depth ? depth : 2, waves);
           break;
         case RTI_I32: st = launch_tile<int32_t>(a, 4, 1, 2, 4); break;
@@ -1085,7 +1217,12 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     const int vec = in_dtype == RTI_U8 ? (k <= 6 ? 16 : 4) : 4;
     const bool vok = vec_ok_for(vec);
     switch (in_dtype) {
-      case RTI_F32: launch_valu<float>(a, vok); break;
+      case RTI_F32:
+        launch_generations(a, es, gens, [vok](const FitArgs& b) {
+          launch_valu<float>(b, vok);
+          return RTI_OK;
+        });
+        break;
       case RTI_I32: launch_valu<int32_t>(a, vok); break;
       default: launch_valu<uint8_t>(a, vok); break;
     }

@@ -58,7 +58,7 @@ constexpr bool fr_stage() { return VEC == 4 && (VEC * K) % 4 == 0 && K <= 9; }
 
 template <int K, int VEC, int NC, int U, typename T, int LAYOUT, bool TAIL>
 __device__ __forceinline__ double fitres_body(const double* __restrict__ A, const double* __restrict__ G, int N,
-                                              const T* __restrict__ src, int64_t P, int64_t lstride,
+                                              const T* __restrict__ src, int64_t P, int64_t pe, int64_t lstride,
                                               float* __restrict__ dst, float* __restrict__ res,
                                               int64_t wave_base, int lane, float* lds_wave) {
   constexpr int CH = 64 * VEC;
@@ -67,7 +67,7 @@ __device__ __forceinline__ double fitres_body(const double* __restrict__ A, cons
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int64_t p0 = wave_base + (int64_t)c * CH + (int64_t)lane * VEC;
-    ok[c] = !TAIL || p0 < P;
+    ok[c] = !TAIL || p0 < pe;
     off[c] = ok[c] ? p0 : 0;  // a chunk past the image re-reads pixel 0 and is neither stored nor summed
   }
   double b[K][NC * VEC], q[NC * VEC];
@@ -159,7 +159,7 @@ __device__ __forceinline__ double fitres_body(const double* __restrict__ A, cons
       if constexpr (fr_stage<K, VEC>()) {
         constexpr int F = VEC * K;
         const int64_t cbase = wave_base + (int64_t)c * CH;
-        if (cbase + CH <= P) {  // wave-uniform: the whole chunk is in the image
+        if (cbase + CH <= pe) {  // wave-uniform: the whole chunk is in the image
 #pragma unroll
           for (int i = 0; i < F; i += 4)
             *reinterpret_cast<floatx4*>(lds_wave + lane * F + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
@@ -189,23 +189,26 @@ __device__ __forceinline__ double fitres_body(const double* __restrict__ A, cons
 template <int K, int VEC, int NC, int U, typename T, int LAYOUT>
 __global__ void __launch_bounds__(FR_THREADS)
 fit_shared_residual_k(const double* __restrict__ A, const double* __restrict__ G, int N, const T* __restrict__ I,
-                      int64_t P, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride,
-                      float* __restrict__ res, double* __restrict__ partial, int64_t pstride) {
+                      int64_t P, int64_t pb, int64_t pe, int64_t lstride, int64_t cstride, float* __restrict__ coef,
+                      int64_t ocstride, float* __restrict__ res, double* __restrict__ partial, int64_t pstride) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   __shared__ double wsum[FR_THREADS / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t wave_base = ((int64_t)blockIdx.x * (FR_THREADS / 64) + wave) * (64 * VEC * NC);
+  // pixels [pb, pe) of P; pb is a multiple of the workgroup's pixel span, so the workgroup's partial slot is
+  // its block index in a one-launch grid
+  const int64_t blk = blockIdx.x + pb / (FR_THREADS * VEC * NC);
+  const int64_t wave_base = (blk * (FR_THREADS / 64) + wave) * (64 * VEC * NC);
   const T* __restrict__ src = I + (int64_t)blockIdx.y * cstride;
   float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
   float* __restrict__ rc = res ? res + (int64_t)blockIdx.y * P : nullptr;
   float* lds_wave = lds_dyn + wave * 64 * VEC * K;
   double mine = 0.0;
-  if (wave_base < P) {  // wave-uniform; idle waves of the last workgroup still join the reduction
-    if (wave_base + (int64_t)(64 * VEC * NC) <= P)
-      mine = fitres_body<K, VEC, NC, U, T, LAYOUT, false>(A, G, N, src, P, lstride, dst, rc, wave_base, lane,
+  if (wave_base < pe) {  // wave-uniform; idle waves of the last workgroup still join the reduction
+    if (wave_base + (int64_t)(64 * VEC * NC) <= pe)
+      mine = fitres_body<K, VEC, NC, U, T, LAYOUT, false>(A, G, N, src, P, pe, lstride, dst, rc, wave_base, lane,
                                                           lds_wave);
     else
-      mine = fitres_body<K, VEC, NC, U, T, LAYOUT, true>(A, G, N, src, P, lstride, dst, rc, wave_base, lane,
+      mine = fitres_body<K, VEC, NC, U, T, LAYOUT, true>(A, G, N, src, P, pe, lstride, dst, rc, wave_base, lane,
                                                          lds_wave);
   }
   if (partial) {
@@ -216,7 +219,7 @@ fit_shared_residual_k(const double* __restrict__ A, const double* __restrict__ G
       double t = 0.0;
 #pragma unroll
       for (int i = 0; i < FR_THREADS / 64; ++i) t += wsum[i];
-      partial[(int64_t)blockIdx.y * pstride + blockIdx.x] = t;
+      partial[(int64_t)blockIdx.y * pstride + blk] = t;
     }
   }
 }
@@ -234,16 +237,18 @@ struct FrArgs {
   double* partial;
   int nc;
   hipStream_t s;
+  int64_t pb = 0, pe = 0;  // this launch's pixel range [pb, pe) (pe 0 = P); pb a multiple of the workgroup span
 };
 
 template <int K, int VEC, int NC, typename T, int LAYOUT>
 int launch_fr_t(const FrArgs& a) {
   constexpr int U = 4;  // loads in flight per lane: the fp64 work per load hides more latency than fp32
-  const dim3 grid(grid_1d(a.P, FR_THREADS * VEC * NC), a.C);
+  const int64_t pe = a.pe ? a.pe : a.P;
+  const dim3 grid(grid_1d(pe - a.pb, FR_THREADS * VEC * NC), a.C);
   const size_t lds =
       (LAYOUT == RTI_COEF_PIXEL_MAJOR && fr_stage<K, VEC>()) ? (size_t)FR_THREADS * VEC * K * sizeof(float) : 0;
   hipLaunchKernelGGL((fit_shared_residual_k<K, VEC, NC, U, T, LAYOUT>), grid, dim3(FR_THREADS), lds, a.s, a.A, a.G,
-                     a.N, static_cast<const T*>(a.I), a.P, a.lstride, a.cstride, a.coef, a.ocstride, a.res, a.partial,
+                     a.N, static_cast<const T*>(a.I), a.P, a.pb, pe, a.lstride, a.cstride, a.coef, a.ocstride, a.res, a.partial,
                      (int64_t)grid_1d(a.P, FR_THREADS));
   return check_launch("rti_fit_shared_residual");
 }
@@ -332,6 +337,28 @@ extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int 
   const bool vec4 = P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 && aligned_to(I, 4 * es) &&
                     (!res || aligned_to(res, 16)) && aligned_to(coef, 16) && a.ocstride % 4 == 0;
   a.nc = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  // launch generations (rti_fit.hip): PTM-6 on 16-B lanes as consecutive launches over pixel ranges of
+  // whole workgroups, each giving every SIMD the same number of waves (2 at 3 or 2 chunks per lane:
+  // 205 / <= 160 VGPRs), AUTO trying 3 then 2 chunks; profiles/r02_fitres_generations_sweep.log
+  int parts = 1;
+  const bool gens = k == 6 && vec4 && a.nc <= 3 && !(kernel & RTI_KERNEL_ONE_LAUNCH);
+  if (gens) {
+    const int64_t slots = 2 * 4 * (int64_t)device_cus();  // waves resident at 2 per SIMD
+    for (int nc : {3, 2}) {
+      if (a.nc && nc != a.nc) continue;
+      const int64_t span = (int64_t)FR_THREADS * 4 * nc, bpc = (P + span - 1) / span;  // workgroups per channel
+      int p = 1;
+      int64_t per = bpc * C * 4;  // waves in one launch
+      if (per > slots) {
+        p = (int)((4 * bpc + slots - 1) / slots);
+        per = 4 * ((bpc + p - 1) / p);
+      }
+      if (p > 1 && (per * 100 < slots * 85 || (double)per * 256 * nc * N * es < 256.0 * (1 << 20))) continue;
+      a.nc = nc;
+      parts = p;
+      break;
+    }
+  }
   if (a.nc == 0) {
     a.nc = 1;
     if (k == 6)
@@ -341,9 +368,30 @@ extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int 
           break;
         }
   }
-  switch (in_dtype) {
-    case RTI_F32: return launch_fr_k<float>(a, vec4);
-    case RTI_U8: return launch_fr_k<uint8_t>(a, vec4);
-    default: return launch_fr_k<int32_t>(a, vec4);
+  auto launch = [&](const FrArgs& b) {
+    switch (in_dtype) {
+      case RTI_F32: return launch_fr_k<float>(b, vec4);
+      case RTI_U8: return launch_fr_k<uint8_t>(b, vec4);
+      default: return launch_fr_k<int32_t>(b, vec4);
+    }
+  };
+  if (parts == 1) return launch(a);
+  const int64_t span = (int64_t)FR_THREADS * 4 * a.nc, units = (P + span - 1) / span;
+  const int64_t per = (units + parts - 1) / parts, pstride = rti_fit_shared_residual_blocks(P);
+  for (int c = 0; c < C; ++c) {
+    FrArgs b = a;
+    b.C = 1;
+    b.I = static_cast<const char*>(I) + (size_t)c * a.cstride * es;
+    b.coef = coef + (size_t)c * a.ocstride;
+    b.res = res ? res + (size_t)c * P : nullptr;
+    b.partial = partial ? partial + (size_t)c * pstride : nullptr;
+    for (int i = 0; i < parts; ++i) {
+      b.pb = i * per * span;
+      b.pe = (i + 1) * per * span < P ? (i + 1) * per * span : P;
+      if (b.pb >= b.pe) break;
+      const int st = launch(b);
+      if (st != RTI_OK) return st;
+    }
   }
+  return RTI_OK;
 }

@@ -14,6 +14,8 @@ namespace rti {
 int fail(int status, const char* fmt, ...);
 // hipGetLastError after a launch -> RTI_OK or RTI_ERR_HIP.
 int check_launch(const char* what);
+// compute units of the current HIP device (cached per device; rti_fit.hip)
+int device_cus();
 
 __host__ __device__ inline bool aligned_to(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 

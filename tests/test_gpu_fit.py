@@ -275,3 +275,34 @@ def test_lds_tile_wide_workgroup(cuda, rc, depth, basis, n):
             for c in range(2):
                 err, ok = coef_close(got[c], ref[c])
                 assert ok, (P, layout, c, err)
+
+
+@pytest.mark.parametrize("basis,N,C,layout", [("ptm", 100, 1, "pixel"), ("ptm", 100, 2, "planar"),
+                                              ("hsh", 40, 1, "pixel"), ("hsh", 40, 2, "planar")])
+def test_launch_generations_bit_identical(cuda, basis, N, C, layout):
+    """AUTO issues large fits as consecutive launches over pixel ranges (rti_fit.hip, launch
+    generations); every pixel's arithmetic is the one-launch kernel's, so the coefficients must be
+    bit-identical to RTI_KERNEL_ONE_LAUNCH's, over a ragged pixel count (partial last wave / tile)."""
+    from rti import _lib as L
+
+    H, W = 2150, 2100  # P = 4 515 000: PTM-6 splits into 5 launches per channel, HSH-16 into 5 tile ranges
+    P = H * W
+    k = rti.basis_terms(basis)
+    g = torch.Generator(device=cuda).manual_seed(7)
+    I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda).to(torch.float32)
+    lu, lv = o.synth_dirs(N, 3)
+    pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=cuda)
+    shape = (C, P, k) if layout == "pixel" else (C, k, P)
+    a = torch.full(shape, float("nan"), device=cuda)
+    b = torch.full(shape, float("nan"), device=cuda)
+    rti.fit_shared_into(pv, I, a, k=k, layout=layout)
+    rti.fit_shared_into(pv, I, b, k=k, layout=layout, flags=L.RTI_KERNEL_ONE_LAUNCH)
+    torch.cuda.synchronize()
+    assert not torch.isnan(a).any()
+    assert torch.equal(a, b)
+    # and against the fp64 oracle on sampled pixels of the last channel (parts' boundaries included)
+    px = np.unique(np.concatenate([np.random.default_rng(5).integers(0, P, 512), [0, P - 1, P // 5, P // 5 - 1]]))
+    ref = o.fit_shared(I[-1][:, torch.as_tensor(px, device=cuda)].cpu().numpy(), o.pinv_shared(basis, lu, lv))
+    got = (a[-1][px] if layout == "pixel" else a[-1][:, px].T).double().cpu().numpy()
+    err, ok = coef_close(got, ref)
+    assert ok, err

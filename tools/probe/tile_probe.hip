@@ -13,7 +13,7 @@ extern "C" int probe_tile_nostore(const float* pinv, int k, int N, const float* 
                           (int)lds) != hipSuccess)
     return 3;
   dim3 grid((unsigned)((P + R - 1) / R), C);
-  hipLaunchKernelGGL(kern, grid, dim3(64 * W), lds, (hipStream_t)stream, pinv, k, N, I, P, P, (int64_t)N * P, coef,
+  hipLaunchKernelGGL(kern, grid, dim3(64 * W), lds, (hipStream_t)stream, pinv, k, N, I, P, (int64_t)0, P, P, (int64_t)N * P, coef,
                      P * k);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

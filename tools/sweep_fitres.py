@@ -50,10 +50,10 @@ def main():
     s = ctypes.c_void_p(stream.cuda_stream)
     vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
-    def fused(nc):
+    def fused(nc, extra=0):
         return lambda: L.check(lib.rti_fit_shared_residual(vp(A64), vp(G), k, N, vp(I), L.RTI_F32, P, C, P, N * P,
                                                            vp(coef), L.RTI_COEF_PIXEL_MAJOR, P * k, vp(res), vp(part),
-                                                           nc << L.RTI_KERNEL_CHUNKS_SHIFT, s), "fused")
+                                                           (nc << L.RTI_KERNEL_CHUNKS_SHIFT) | extra, s), "fused")
 
     def fit():
         L.check(lib.rti_fit_shared(vp(pv), k, N, vp(I), L.RTI_F32, P, C, P, N * P, vp(coef), L.RTI_COEF_PIXEL_MAJOR,
@@ -64,6 +64,20 @@ def main():
                                      P * k, vp(res), vp(part), s), "resid")
 
     variants = [(f"fused_nc{nc}", fused(nc)) for nc in map(int, args.chunks.split(","))]
+    # launch generations (RTI_KERNEL_ONE_LAUNCH = the pre-generation single launch)
+    variants += [(f"fused_nc{nc}_one_launch", fused(nc, L.RTI_KERNEL_ONE_LAUNCH)) for nc in (2, 3)]
+    variants += [("fused_auto", fused(0))]
+    outs = {}
+    for name, fn in variants:
+        if name in ("fused_auto", "fused_nc3_one_launch", "fused_nc2", "fused_nc2_one_launch"):
+            part.zero_()
+            fn()
+            torch.cuda.synchronize()
+            outs[name] = (coef.clone(), res.clone(), part.sum(1).clone())
+    for name in outs:
+        same = all(torch.equal(x, y) for x, y in zip(outs[name][:2], outs["fused_nc3_one_launch"][:2]))
+        print(f"{name}: coef/res bit-identical to fused_nc3_one_launch: {same}; residual energy "
+              f"{outs[name][2].tolist()} vs {outs['fused_nc3_one_launch'][2].tolist()}", flush=True)
     variants += [("fit_only", fit), ("residual_only", resid)]
     for _, fn in variants:
         for _ in range(3):
