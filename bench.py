@@ -164,7 +164,8 @@ def load_traffic(workload_key):
     try:
         with open(path) as f:
             entry = json.load(f).get(workload_key) or {}
-        return entry.get("traffic_bytes_per_launch")
+        # per step: launch generations split one step into launches_per_step launches
+        return entry.get("traffic_bytes_per_step", entry.get("traffic_bytes_per_launch"))
     except (OSError, ValueError):
         return None
 
@@ -209,11 +210,18 @@ class Workload:
 
     dtype = "f32"
 
+    launches = 1  # kernel launches per step (fits: rti_last_launch_count after a step, launch generations)
+
     def roofline(self, kernel_ms):
+        """achieved = algorithmic bytes of one step / the step's kernel time (event-timed on the launch
+        stream; with L > 1 launch generations per step that time includes the L - 1 launch boundaries,
+        and rocprofv3's per-launch average x L is the gap-free figure)."""
         gbs = self.alg_bytes / (kernel_ms * 1e-3) / 1e9
+        L = int(self.launches)
         return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": self.traffic(), "kernel_ms": round(kernel_ms, 4),
-                "alg_bytes_per_launch": self.alg_bytes}
+                "alg_bytes_per_launch": self.alg_bytes / L, "alg_bytes_per_step": self.alg_bytes,
+                "launches_per_step": L, "kernel_ms_per_launch": round(kernel_ms / L, 5)}
 
     def traffic(self):
         return None
@@ -263,6 +271,8 @@ class FitWorkload(Workload):
                 L.check(st, "rti_fit_shared")
 
         self.step = step
+        step(0)
+        self.launches = int(L.lib().rti_last_launch_count())
 
     def traffic(self):
         if self.ctx.world != 1 or self.ctx.weak:
@@ -333,6 +343,8 @@ class FitResidualWorkload(FitWorkload):
                 L.check(st, "rti_fit_shared_residual")
 
         self.step = step
+        step(0)
+        self.launches = int(L.lib().rti_last_launch_count())
         self.dtype = "f32 in / f64 accumulate / f32 out"
 
     def traffic(self):

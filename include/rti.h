@@ -92,6 +92,10 @@ typedef void* rti_stream_t; /* hipStream_t */
 int         rti_version(void);                 /* 10000*major + 100*minor + patch */
 const char* rti_status_string(int status);
 const char* rti_last_error(void);
+/* Kernel launches issued by this thread's most recent rti_fit_shared / rti_fit_shared_residual call:
+ * 1, or more when AUTO issues a large fit as consecutive "launch generations" over pixel ranges
+ * (rti_fit.hip).  For timing tools (per-launch figures); the results do not depend on it. */
+int rti_last_launch_count(void);
 int         rti_basis_terms(int basis);        /* k for a basis, or -1 */
 int         rti_device_count(void);            /* hipGetDeviceCount, 0 on failure */
 

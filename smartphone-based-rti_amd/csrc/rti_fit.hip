@@ -1060,6 +1060,7 @@ Generations tile_generations(const FitArgs& a, int64_t tile_px) {
 template <typename F>
 int launch_generations(const FitArgs& a, size_t es, const Generations& g, F&& launch) {
   if (!g.split) return launch(a);
+  int launches = 0;
   const int64_t units = (a.P + g.unit - 1) / g.unit, per = (units + g.parts - 1) / g.parts;
   for (int c = 0; c < a.C; ++c) {
     FitArgs b = a;
@@ -1072,6 +1073,7 @@ int launch_generations(const FitArgs& a, size_t es, const Generations& g, F&& la
       if (b.pb >= b.pe) break;
       const int st = launch(b);
       if (st != RTI_OK) return st;
+      note_launches(++launches);
     }
   }
   return RTI_OK;
@@ -1093,6 +1095,7 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: input dtype %d", in_dtype);
   if (coef_layout != RTI_COEF_PIXEL_MAJOR && coef_layout != RTI_COEF_PLANAR)
     return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: coef layout %d", coef_layout);
+  note_launches(1);
   FitArgs a;
   a.pinv = pinv;
   a.k = k;

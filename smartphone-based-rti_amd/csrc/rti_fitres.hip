@@ -313,6 +313,7 @@ extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int 
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_residual: input dtype %d", in_dtype);
   if (coef_layout != RTI_COEF_PIXEL_MAJOR && coef_layout != RTI_COEF_PLANAR)
     return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: coef layout %d", coef_layout);
+  note_launches(1);
   FrArgs a;
   a.A = A;
   a.G = ginv;
@@ -338,25 +339,33 @@ extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int 
                     (!res || aligned_to(res, 16)) && aligned_to(coef, 16) && a.ocstride % 4 == 0;
   a.nc = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
   // launch generations (rti_fit.hip): PTM-6 on 16-B lanes as consecutive launches over pixel ranges of
-  // whole workgroups, each giving every SIMD the same number of waves (2 at 3 or 2 chunks per lane:
-  // 205 / <= 160 VGPRs), AUTO trying 3 then 2 chunks; profiles/r02_fitres_generations_sweep.log
+  // whole workgroups, each giving the SIMDs one or two waves (3 or 2 chunks per lane: 205 / <= 160
+  // VGPRs, two waves resident per SIMD); profiles/r02_generations_sweep.log
   int parts = 1;
   const bool gens = k == 6 && vec4 && a.nc <= 3 && !(kernel & RTI_KERNEL_ONE_LAUNCH);
   if (gens) {
-    const int64_t slots = 2 * 4 * (int64_t)device_cus();  // waves resident at 2 per SIMD
+    // efficiency of a launch = its waves / (SIMDs x the waves of the busiest SIMD); AUTO takes the
+    // better-balanced of 3 and 2 chunks (3 unless 2 is > 3 points better): c3 as 6 launches of 1800
+    // waves at 3 chunks 0.5835 ms, 8 launches of 2025 at 2 chunks 0.5775, one launch 0.6155
+    const int64_t simds = 4 * (int64_t)device_cus();
+    double best = 0.0;
+    const int want = a.nc;  // explicit chunks (0 = AUTO)
     for (int nc : {3, 2}) {
-      if (a.nc && nc != a.nc) continue;
+      if (want && nc != want) continue;
       const int64_t span = (int64_t)FR_THREADS * 4 * nc, bpc = (P + span - 1) / span;  // workgroups per channel
       int p = 1;
       int64_t per = bpc * C * 4;  // waves in one launch
-      if (per > slots) {
-        p = (int)((4 * bpc + slots - 1) / slots);
+      if (per > 2 * simds) {
+        p = (int)((4 * bpc + 2 * simds - 1) / (2 * simds));
         per = 4 * ((bpc + p - 1) / p);
       }
-      if (p > 1 && (per * 100 < slots * 85 || (double)per * 256 * nc * N * es < 256.0 * (1 << 20))) continue;
-      a.nc = nc;
-      parts = p;
-      break;
+      const double eff = (double)per / (double)(((per + simds - 1) / simds) * simds);
+      if (eff < 0.85 || (p > 1 && (double)per * 256 * nc * N * es < 256.0 * (1 << 20))) continue;
+      if (eff > best + 0.03) {
+        best = eff;
+        a.nc = nc;
+        parts = p;
+      }
     }
   }
   if (a.nc == 0) {
@@ -391,6 +400,7 @@ extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int 
       if (b.pb >= b.pe) break;
       const int st = launch(b);
       if (st != RTI_OK) return st;
+      note_launches(c * parts + i + 1);
     }
   }
   return RTI_OK;

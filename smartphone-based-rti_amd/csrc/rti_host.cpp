@@ -19,6 +19,9 @@
 namespace rti {
 
 thread_local char g_last_error[512] = "";
+thread_local int g_launches = 0;
+
+void note_launches(int n) { g_launches = n; }
 
 int fail(int status, const char* fmt, ...) {
   va_list ap;
@@ -204,6 +207,8 @@ const char* rti_status_string(int status) {
 }
 
 const char* rti_last_error(void) { return g_last_error; }
+
+int rti_last_launch_count(void) { return g_launches; }
 
 int rti_basis_terms(int basis) { return basis_terms(basis); }
 

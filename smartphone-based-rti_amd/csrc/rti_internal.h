@@ -16,6 +16,8 @@ int fail(int status, const char* fmt, ...);
 int check_launch(const char* what);
 // compute units of the current HIP device (cached per device; rti_fit.hip)
 int device_cus();
+// records the kernel launches of the current C-ABI call (rti_last_launch_count)
+void note_launches(int n);
 
 __host__ __device__ inline bool aligned_to(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 

@@ -6,7 +6,7 @@ WRITE_SIZE --pmc passes, with the gfx950 correction of MI355X_MICROARCH.md
 units are KiB: ×1024).
 
   python tools/summarize_prof.py --trace DIR --fetch DIR --write DIR --kernel REGEX
-        --key WORKLOAD --alg-bytes B [--out profiles/traffic.json]
+        --key WORKLOAD --alg-bytes B (per bench step) [--launches-per-step L] [--out profiles/traffic.json]
 """
 import argparse
 import csv
@@ -33,9 +33,13 @@ def main():
     ap.add_argument("--key", required=True)
     ap.add_argument("--alg-bytes", type=float, required=True)
     ap.add_argument("--out", default="profiles/traffic.json")
+    ap.add_argument("--launches-per-step", type=int, default=1,
+                    help="kernel launches per bench step (launch generations): per-step figures = per-launch x L")
     args = ap.parse_args()
     rx = re.compile(args.kernel)
-    summary = {"kernel_regex": args.kernel, "alg_bytes_per_launch": args.alg_bytes}
+    L = args.launches_per_step
+    summary = {"kernel_regex": args.kernel, "alg_bytes_per_launch": args.alg_bytes / L, "launches_per_step": L,
+               "alg_bytes_per_step": args.alg_bytes}
     if args.trace:
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows(args.trace, "kernel_trace.csv")
                 if rx.search(r["Kernel_Name"])]
@@ -53,7 +57,8 @@ def main():
     if "FETCH_SIZE_bytes_corrected" in summary and "WRITE_SIZE_bytes_corrected" in summary:
         summary["traffic_bytes_per_launch"] = summary["FETCH_SIZE_bytes_corrected"] + \
             summary["WRITE_SIZE_bytes_corrected"]
-        summary["traffic_over_alg"] = summary["traffic_bytes_per_launch"] / args.alg_bytes
+        summary["traffic_bytes_per_step"] = summary["traffic_bytes_per_launch"] * L
+        summary["traffic_over_alg"] = summary["traffic_bytes_per_step"] / args.alg_bytes
     data = {}
     if os.path.exists(args.out):
         with open(args.out) as fh:
