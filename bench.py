@@ -2,8 +2,8 @@
 """Benchmark of the shared-direction PTM fit (BASELINE.json metric) and the other §8 rows.
 
 Metric: Mpix·lights/s of the 6-coefficient PTM fit on a 3840×2160 × 100-light fp32 stack
-(BASELINE.json configs[2], "at 1/2/4/8 GPU").  One step = one rti_fit_shared launch per rank
-over that rank's row block, inputs resident in HBM.
+(BASELINE.json configs[2], "at 1/2/4/8 GPU").  One step = one rti_fit_shared call per rank over that
+rank's row block (AUTO issues it as launches_per_step launch generations), inputs resident in HBM.
 
 Multi-GPU: one process per GPU.  ``--gpus N`` without WORLD_SIZE in the
 environment re-launches this script under ``torch.distributed.run`` with N ranks (before the
@@ -228,7 +228,7 @@ class Workload:
 
 
 class FitWorkload(Workload):
-    """One step = one rti_fit_shared launch over this rank's row block of the stack."""
+    """One step = one rti_fit_shared call (launches_per_step launches) over this rank's row block."""
 
     def __init__(self, args, cfg, ctx):
         import torch
@@ -311,7 +311,7 @@ class FitWorkload(Workload):
 
 
 class FitResidualWorkload(FitWorkload):
-    """One step = one rti_fit_shared_residual launch: coefficients + per-pixel RMS residuals + per-workgroup
+    """One step = one rti_fit_shared_residual call: coefficients + per-pixel RMS residuals + per-workgroup
     residual energy in one pass over the stack (fp64 accumulation)."""
 
     def __init__(self, args, cfg, ctx):
