@@ -50,7 +50,8 @@ def main():
         opts = parts[2].split("+") if len(parts) > 2 else []
         fl = (rti._lib.RTI_KERNEL_NONTEMPORAL if "nt" in opts else 0) | \
              (rti._lib.RTI_KERNEL_PINV_LDS if "lds" in opts else 0) | \
-             (rti._lib.RTI_KERNEL_NT_STORE if "nts" in opts else 0) | (rti._lib.RTI_KERNEL_STAGE if "stage" in opts else 0)
+             (rti._lib.RTI_KERNEL_NT_STORE if "nts" in opts else 0) | (rti._lib.RTI_KERNEL_STAGE if "stage" in opts else 0) | \
+             (rti._lib.RTI_KERNEL_ONE_LAUNCH if "one" in opts else 0)
         for o in opts:  # c<n>: chunks per lane (rti.h RTI_KERNEL_CHUNKS)
             if o[:1] == "c" and o[1:].isdigit():
                 fl |= int(o[1:]) << 12
