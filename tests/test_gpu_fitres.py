@@ -147,3 +147,45 @@ def test_full_size_4k_n100(cuda):
     assert abs(float(rms) ** 2 - mean_sq) <= 1e-6 * mean_sq
     expect = np.sqrt(4.0 + 1.0 / 12.0) * np.sqrt((n - 6) / n)  # N(0, 2²) noise + rounding
     assert abs(float(rms) - expect) < 0.02 * expect
+
+
+@pytest.mark.parametrize("layout", ["pixel", "planar"])
+def test_launch_generations_bit_identical(cuda, layout):
+    """AUTO issues a large fit + residual call as consecutive launches over pixel ranges of whole
+    workgroups (launch generations, rti_fitres.hip); coefficients, residuals and the per-workgroup
+    residual energies must equal RTI_KERNEL_ONE_LAUNCH's bit for bit (same chunks per lane here), over a
+    ragged pixel count and 2 channels, and match the fp64 oracle on sampled pixels."""
+    import ctypes
+
+    from rti import _lib as L
+
+    H, W, N, C, k = 2150, 2100, 100, 2, 6  # P = 4 515 000: 3 chunks per lane, 3 launches per channel
+    P = H * W
+    lu, lv = o.synth_dirs(N, 9)
+    g = torch.Generator(device=cuda).manual_seed(11)
+    I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda).to(torch.float32)
+    A64 = torch.as_tensor(rti.design_matrix(lu, lv, "ptm"), device=cuda).contiguous()
+    G = torch.as_tensor(rti.gram_inverse(lu, lv, "ptm"), device=cuda).contiguous()
+    lib = L.lib()
+    nb = int(lib.rti_fit_shared_residual_blocks(P))
+    s = ctypes.c_void_p(torch.cuda.current_stream(cuda).cuda_stream)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    outs = []
+    for flags in (0, L.RTI_KERNEL_ONE_LAUNCH):
+        coef = torch.full((C, P, k) if layout == "pixel" else (C, k, P), float("nan"), device=cuda)
+        res = torch.full((C, P), float("nan"), device=cuda)
+        part = torch.zeros((C, nb), dtype=torch.float64, device=cuda)
+        st = lib.rti_fit_shared_residual(vp(A64), vp(G), k, N, vp(I), L.RTI_F32, P, C, P, N * P, vp(coef),
+                                         rti.api._layout_id(layout), P * k, vp(res), vp(part), flags, s)
+        L.check(st, "rti_fit_shared_residual")
+        outs.append((coef, res, part, int(lib.rti_last_launch_count())))
+    torch.cuda.synchronize()
+    (ca, ra, pa, la), (cb, rb, pb, lb) = outs
+    assert la > 1 and lb == 1, (la, lb)
+    assert not torch.isnan(ca).any() and not torch.isnan(ra).any()
+    assert torch.equal(ca, cb) and torch.equal(ra, rb) and torch.equal(pa, pb)
+    px = np.unique(np.concatenate([np.random.default_rng(3).integers(0, P, 256), [0, P - 1, P // 3, P // 3 - 1]]))
+    idx = torch.as_tensor(px, device=cuda)
+    for c in range(C):
+        cc = ca[c][idx] if layout == "pixel" else ca[c][:, idx].T
+        check(cc.cpu().numpy(), ra[c][idx].cpu().numpy(), None, I[c][:, idx].double().cpu().numpy(), "ptm", lu, lv, k)
