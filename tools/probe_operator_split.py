@@ -46,7 +46,23 @@ def main():
                 L.check(st, "rti_apply_operator_f16")
         return f
 
-    variants = [(f"operator {p} launch(es)", parts_fn(p)) for p in (1, 2, 3, 4, 5)]
+    variants = [(f"operator {p} launch(es)", parts_fn(p)) for p in (1, 2)]
+    plib = os.path.join(ROOT, "tools", "probe", "libop_probe.so")
+    if os.path.exists(plib):  # explicit row split gy: launches of T tiles x gy row groups (one generation ~ 512 WGs)
+        probe = ctypes.CDLL(plib)
+        probe.probe_op.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+
+        def gen_fn(T, gy):
+            def f():
+                for a0 in range(0, P, 128 * T):
+                    np_ = min(P - a0, 128 * T)
+                    assert probe.probe_op(vp(wl.hi), vp(wl.lo), wl.Kp, wl.inv, E, N, vp(wl.I), P, a0, np_, gy,
+                                          vp(wl.out), wl.stream) == 0
+            return f
+        for T, gy in ((1250, 2), (1250, 1), (256, 2), (512, 1), (128, 4), (250, 2), (625, 2)):
+            variants.append((f"probe T={T} gy={gy}", gen_fn(T, gy)))
     ref = None
     for n, f in variants:
         wl.out.zero_()
