@@ -1014,7 +1014,9 @@ struct Generations {
 // balanced split; the >= 1000-wave rule applies).
 int valu_generations(const FitArgs& a, size_t es, Generations& g) {
   const int64_t simds = 4 * (int64_t)device_cus();
-  auto balanced = [&](int64_t w) { return (w * 100 >= simds * 85 && w <= simds) || (w * 100 >= simds * 170 && w <= 2 * simds); };
+  auto balanced = [&](int64_t w) {  // every SIMD one wave (>= 85 % of them busy) or two (>= 85 % with two)
+    return (w * 100 >= simds * 85 && w <= simds) || (w * 100 >= simds * 170 && w <= 2 * simds);
+  };
   for (int nc : {4, 8, 2}) {
     const int64_t ppw = 256 * nc, wpc = (a.P + ppw - 1) / ppw, total = wpc * a.C;
     Generations t;
@@ -1192,7 +1194,8 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
       switch (in_dtype) {
         case RTI_F32:
           if (tile_auto && !(kernel & RTI_KERNEL_ONE_LAUNCH)) gens = tile_generations(a, 4096);
-          st = tile_auto ? launch_generations(a, es, gens, [](const FitArgs& b) { return launch_tile<float>(b, 15, 1, 1, 8); })
+          st = tile_auto ? launch_generations(a, es, gens,
+                                              [](const FitArgs& b) { return launch_tile<float>(b, 15, 1, 1, 8); })
                          : launch_tile<float>(a, rc0, sp ? sp : 2, depth ? depth : 2, waves);
           break;
         case RTI_I32: st = launch_tile<int32_t>(a, 4, 1, 2, 4); break;
