@@ -22,6 +22,7 @@
 //    still 256 contiguous bytes per 16 lanes.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <type_traits>
 
@@ -32,15 +33,15 @@ namespace rti {
 
 // compute units of the current device (cached; 256 on MI355X)
 int device_cus() {
-  static int cache[64];
+  static std::atomic<int> cache[64];  // 0 = not queried yet (concurrent first queries store the same value)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cache[dev] <= 0) {
-    int n = 0;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cache[dev] = n;
+    cache[dev].store(n, std::memory_order_relaxed);
   }
-  return cache[dev];
+  return n;
 }
 
 namespace {
