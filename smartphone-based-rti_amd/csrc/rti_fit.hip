@@ -1193,12 +1193,17 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
       const int rc0 = rc ? rc : (N <= 512 ? 8 : 4);
       int st;
       switch (in_dtype) {
-        case RTI_F32:
-          if (tile_auto && !(kernel & RTI_KERNEL_ONE_LAUNCH)) gens = tile_generations(a, 4096);
-          st = tile_auto ? launch_generations(a, es, gens,
-                                              [](const FitArgs& b) { return launch_tile<float>(b, 15, 1, 1, 8); })
-                         : launch_tile<float>(a, rc0, sp ? sp : 2, depth ? depth : 2, waves);
+        case RTI_F32: {
+          // launch generations for the 4096-pixel tile_w kernels (AUTO, or explicit 8 / 4 waves at rc >= 12:
+          // one workgroup per CU); the other tile forms stay one launch
+          const bool w4096 = tile_auto || ((waves == 8 || waves == 4) && rc >= 12);
+          if (w4096 && !(kernel & RTI_KERNEL_ONE_LAUNCH)) gens = tile_generations(a, 4096);
+          st = launch_generations(a, es, gens, [&](const FitArgs& b) {
+            return tile_auto ? launch_tile<float>(b, 15, 1, 1, 8)
+                             : launch_tile<float>(b, rc0, sp ? sp : 2, depth ? depth : 2, waves);
+          });
           break;
+        }
         case RTI_I32: st = launch_tile<int32_t>(a, 4, 1, 2, 4); break;
         default: st = launch_tile<uint8_t>(a, 4, 1, 2, 4); break;
       }
