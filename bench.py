@@ -431,6 +431,12 @@ class RelightWorkload(Workload):
             r["bound"] = "l3"  # the maps stay in the 256 MiB Infinity Cache between launches
         return r
 
+    def traffic(self):
+        # PMC bytes per launch of the cold (HBM-streamed) case, profiles/traffic.json (tools/pmc_pass.sh)
+        if self.ctx.world != 1 or self.ctx.weak or not self.cold():
+            return None
+        return load_traffic(self.args.config)
+
     def parity(self):
         import torch
 
@@ -522,6 +528,11 @@ class PerPixelWorkload(Workload):
     """One step = one rti_fit_perpixel_cam launch (directions from cameras, fp64 normal equations)."""
 
     dtype = "f32 in / f64 solve"
+
+    def traffic(self):
+        if self.ctx.world != 1 or self.ctx.weak:
+            return None
+        return load_traffic(self.args.config)
 
     def __init__(self, args, cfg, ctx):
         import torch

@@ -296,7 +296,9 @@ def test_launch_generations_bit_identical(cuda, basis, N, C, layout):
     a = torch.full(shape, float("nan"), device=cuda)
     b = torch.full(shape, float("nan"), device=cuda)
     rti.fit_shared_into(pv, I, a, k=k, layout=layout)
+    assert int(L.lib().rti_last_launch_count()) > 1  # the call was split into launch generations
     rti.fit_shared_into(pv, I, b, k=k, layout=layout, flags=L.RTI_KERNEL_ONE_LAUNCH)
+    assert int(L.lib().rti_last_launch_count()) == 1
     torch.cuda.synchronize()
     assert not torch.isnan(a).any()
     assert torch.equal(a, b)
