@@ -1006,7 +1006,7 @@ struct Generations {
   int64_t unit = 1;    // pixels per wave (VALU) or per workgroup tile; part bounds are multiples of it
 };
 
-// VALU stream (PTM-6 fp32, AUTO): chunks per lane nc and launches such that every launch gives
+// VALU stream (PTM-6 fp32 / int32, AUTO): chunks per lane nc and launches such that every launch gives
 // every SIMD the same number of waves, one or two (all resident at once: one generation), trying
 // nc = 4, 8, 2 in that order.  Two boxes agreed on nc = 4 (c3 as 4 launches of 2025 waves: 0.533 and
 // 0.534 ms, against 0.562 / 0.597 for one launch at nc = 8); 8 chunks at one wave per SIMD ran
@@ -1154,23 +1154,25 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     // shard 4 (1012 waves) 0.0675 vs 2 0.0679 vs 8 (506 waves) 0.0950 ms.  HSH-16 measured no
     // gain (c4: 3.88 ms at 1 and 2 chunks, 4.57 at 3) and keeps one chunk, as do the
     // LDS-weight tuning variants.
-    // r02: fp32 AUTO picks nc and the launch generations together (valu_generations above).
+    // r02: AUTO picks nc and the launch generations together for 4-byte stacks (valu_generations
+    // above; c3 fp32 0.593 -> 0.532 ms, int32 0.651 -> 0.532 ms).  8-bit stacks keep one launch of
+    // one-chunk 16-pixel lanes: their 2-chunk generations ran 0.366 against 0.244 ms
+    // (profiles/r02_generations_sweep.log).
     const bool plain = (a.mode & ~(VM_NT | VM_NTS | VM_STAGE | VM_ROT)) == 0;
     a.nc = 1;
-    if (plain && in_dtype != RTI_U8 && k == 6) {
-      int gnc = 0;
-      if (sel == RTI_KERNEL_AUTO && in_dtype == RTI_F32 && !(kernel & RTI_KERNEL_ONE_LAUNCH) && vec_ok_for(4))
-        gnc = valu_generations(a, es, gens);
-      if (gnc) {
-        a.nc = gnc;
-      } else {
-        const int64_t groups = P * C / 4;  // 4-pixel lane groups
-        for (int nc = 8; nc > 1; nc >>= 1)
-          if (groups / (64 * nc) >= 1000) {
-            a.nc = nc;
-            break;
-          }
-      }
+    int gnc = 0;
+    if (plain && k == 6 && in_dtype != RTI_U8 && sel == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_ONE_LAUNCH) &&
+        vec_ok_for(4))
+      gnc = valu_generations(a, es, gens);
+    if (gnc) {
+      a.nc = gnc;
+    } else if (plain && in_dtype != RTI_U8 && k == 6) {
+      const int64_t groups = P * C / 4;  // 4-pixel lane groups
+      for (int nc = 8; nc > 1; nc >>= 1)
+        if (groups / (64 * nc) >= 1000) {
+          a.nc = nc;
+          break;
+        }
     }
   }
   const bool mfma_ok = N <= 1024 && P % 4 == 0 && a.lstride % 4 == 0 && a.cstride % 4 == 0 &&
@@ -1235,7 +1237,12 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
           return RTI_OK;
         });
         break;
-      case RTI_I32: launch_valu<int32_t>(a, vok); break;
+      case RTI_I32:
+        launch_generations(a, es, gens, [vok](const FitArgs& b) {
+          launch_valu<int32_t>(b, vok);
+          return RTI_OK;
+        });
+        break;
       default: launch_valu<uint8_t>(a, vok); break;
     }
   }

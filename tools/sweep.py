@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--store-windows", default="", help="PTM-6 store probe wrapping its stores inside W MiB (list)")
     ap.add_argument("--rows", type=int, default=0, help="override the config's H (row-shard sizes: 2160/G)")
+    ap.add_argument("--in-dtype", default="f32", choices=["f32", "u8", "i32"], help="intensity stack type")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     _, H, W, N, C, basis, desc = bench.CONFIGS[args.config]
@@ -42,6 +43,8 @@ def main():
     P = H * W
     lu, lv = bench.synth_dirs(N, 2)
     I = bench.synth_stack(H, W, N, C, basis, lu, lv, 1000, dev)
+    if args.in_dtype != "f32":  # integer-valued 0..255 stacks, as the reference's V channel
+        I = I.to(torch.uint8 if args.in_dtype == "u8" else torch.int32)
     pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=dev)
     coefs = {"pixel": torch.empty((C, P, k), device=dev), "planar": torch.empty((C, k, P), device=dev)}
     variants = []
