@@ -104,8 +104,10 @@ __device__ __forceinline__ void store_f32_nt(float* __restrict__ dst, const floa
   }
 }
 
+// pixel-major stores staged through a per-wave LDS slab of 64 lanes x 4 pixels x K floats: 4-pixel
+// lanes in one step, 16-pixel (u8) lanes in four steps of 16 lanes each
 template <int K, int VEC>
-constexpr bool stage_ok() { return VEC == 4 && (VEC * K) % 4 == 0 && K <= 9; }
+constexpr bool stage_ok() { return (VEC == 4 || VEC == 16) && K <= 9; }
 
 // Lane → pixel map.  A wave owns NC·64·VEC consecutive pixels; lane l's chunk c is the VEC
 // pixels at wave_base + c·64·VEC + l·VEC, so each load instruction of the wave reads 64·VEC
@@ -215,26 +217,39 @@ __device__ __forceinline__ void fit_valu_body(const float* __restrict__ pinv, in
 #pragma unroll
         for (int k = 0; k < K; ++k) o[v * K + k] = acc[k][c * VEC + v];
       if constexpr (STAGE) {
-        constexpr int F = VEC * K;  // floats per lane (24 for PTM-6)
+        constexpr int F4 = 4 * K;      // floats of a 4-pixel group (24 for PTM-6)
+        constexpr int SUB = VEC / 4;   // steps: 1, or 4 for 16-pixel u8 lanes (16 lanes = 256 pixels each)
+        constexpr int LPS = 64 / SUB;  // lanes per step
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         const int64_t cbase = wave_base + (int64_t)c * CH;  // the wave's first pixel of chunk c
-        if (cbase + CH <= pe) {  // wave-uniform: the whole chunk's 64*F floats are in range
+        if (cbase + CH <= pe) {  // wave-uniform: the whole chunk's CH*K floats are in range
           const int woff = LDSW ? ((N * KP + 3) & ~3) : 0;
-          float* st = lds_dyn + woff + wave * 64 * F;
+          float* st = lds_dyn + woff + wave * 64 * F4;
 #pragma unroll
-          for (int i = 0; i < F; i += 4)
-            *reinterpret_cast<floatx4*>(st + lane * F + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          float* wdst = dst + cbase * K;
+          for (int q = 0; q < SUB; ++q) {
+            if (SUB == 1 || lane / LPS == q) {  // this step's lanes park their VEC pixels' rows
+              float* ls = st + (lane % LPS) * (VEC * K);
 #pragma unroll
-          for (int j = 0; j < F / 4; ++j) {
-            const floatx4 t = *reinterpret_cast<const floatx4*>(st + j * 256 + lane * 4);
-            if constexpr (NTS)
-              __builtin_nontemporal_store(t, reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4));
-            else
-              *reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4) = t;
+              for (int i = 0; i < VEC * K; i += 4)
+                *reinterpret_cast<floatx4*>(ls + i) = floatx4{o[i], o[i + 1], o[i + 2], o[i + 3]};
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            float* wdst = dst + (cbase + (int64_t)q * 256) * K;  // 256 pixels' rows, 1 KiB per instruction
+#pragma unroll
+            for (int j = 0; j < F4 / 4; ++j) {
+              const floatx4 t = *reinterpret_cast<const floatx4*>(st + j * 256 + lane * 4);
+              if constexpr (NTS)
+                __builtin_nontemporal_store(t, reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4));
+              else
+                *reinterpret_cast<floatx4*>(wdst + j * 256 + lane * 4) = t;
+            }
+            if constexpr (SUB > 1) {  // the slab is rewritten by the next step
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
           }
           continue;
         }
@@ -743,7 +758,7 @@ void launch_valu_t(const FitArgs& a) {
   constexpr int KP = (K + 3) & ~3;
   size_t lds = (MODE & VM_LDS) ? (((size_t)a.N * KP + 3) & ~(size_t)3) * sizeof(float) : 0;
   if constexpr ((MODE & VM_STAGE) && LAYOUT == RTI_COEF_PIXEL_MAJOR && stage_ok<K, VEC>())
-    lds += (size_t)4 * 64 * VEC * K * sizeof(float);
+    lds += (size_t)4 * 64 * 4 * K * sizeof(float);  // 4 waves x 64 lanes x 4 pixels x K
   hipLaunchKernelGGL((fit_shared_valu<K, VEC, NC, T, LAYOUT, MODE>), grid, dim3(256), lds, a.stream, a.pinv, a.N,
                      static_cast<const T*>(a.I), a.P, a.pb, pe, a.lstride, a.cstride, a.coef, a.ocstride);
 }
@@ -797,6 +812,11 @@ void launch_valu_m(const FitArgs& a) {
 #undef RTI_MODE_CASE
     }
   } else {
+    // 16-pixel u8 lanes: PTM-6 pixel-major stores staged through LDS (AUTO's VM_STAGE) as for fp32
+    if constexpr (VEC == 16 && K == 6 && LAYOUT == RTI_COEF_PIXEL_MAJOR) {
+      if ((a.mode & (VM_NT | VM_STAGE)) == (VM_NT | VM_STAGE))
+        return launch_valu_t<K, VEC, 1, T, LAYOUT, VM_NT | VM_STAGE>(a);
+    }
     if (a.mode & VM_NT)
       launch_valu_t<K, VEC, 1, T, LAYOUT, VM_NT>(a);
     else

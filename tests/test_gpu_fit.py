@@ -308,3 +308,25 @@ def test_launch_generations_bit_identical(cuda, basis, N, C, layout):
     got = (a[-1][px] if layout == "pixel" else a[-1][:, px].T).double().cpu().numpy()
     err, ok = coef_close(got, ref)
     assert ok, err
+
+
+@pytest.mark.parametrize("P", [1024 * 37, 1024 * 37 + 16 * 5, 4096 * 600 + 48])
+def test_u8_staged_pixel_major_matches_planar(cuda, P):
+    """8-bit stacks (the reference's V channel, analysis.py:219): AUTO's 16-pixel lanes leave their
+    pixel-major coefficients through the LDS slab in four 256-pixel steps (whole 1024-pixel chunks; the
+    partial chunk stores directly).  Same accumulators as the planar layout's direct stores, so the two
+    must agree bit for bit, and with the fp64 oracle."""
+    N = 40
+    lu, lv = o.synth_dirs(N, 5)
+    g = torch.Generator(device=cuda).manual_seed(P)
+    I = torch.randint(0, 256, (N, P), generator=g, device=cuda).to(torch.uint8)
+    pv = torch.as_tensor(rti.pinv(lu, lv, "ptm").astype(np.float32), device=cuda)
+    a = torch.full((1, P, 6), float("nan"), device=cuda)
+    b = torch.full((1, 6, P), float("nan"), device=cuda)
+    rti.fit_shared_into(pv, I, a, k=6, layout="pixel")
+    rti.fit_shared_into(pv, I, b, k=6, layout="planar")
+    assert torch.equal(a[0], b[0].T)
+    idx = np.unique(np.concatenate([np.random.default_rng(1).integers(0, P, 300), [0, 255, 256, 1023, P - 1]]))
+    ref = o.fit_shared(I[:, torch.as_tensor(idx, device=cuda)].cpu().numpy(), o.pinv_shared("ptm", lu, lv))
+    err, ok = coef_close(a[0][idx].double().cpu().numpy(), ref)
+    assert ok, err
