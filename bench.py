@@ -865,6 +865,15 @@ def allgather_legs(wl, ctx, reps=5):
     return gather_ms, e2e_ms, chunks
 
 
+def device_info(dev):
+    """The box this line was measured on (box-to-box spread is ~±6 %)."""
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    return {"name": p.name, "arch": getattr(p, "gcnArchName", ""), "cus": p.multi_processor_count,
+            "hbm_GiB": round(p.total_memory / 2 ** 30, 1)}
+
+
 def reduce_max(vals, ctx, backend):
     import torch
     import torch.distributed as dist
@@ -1053,6 +1062,7 @@ def main():
                                 "per_rank_median": [round(x, 5) for x in kernel_ms_rank]},
             "parity": parity,
             "cpu_baseline": cpu,
+            "device": device_info(dev),
         }
         if gather_ms is not None:
             line["allgather_ms"] = round(gather_ms, 3)
