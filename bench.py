@@ -311,8 +311,9 @@ class FitWorkload(Workload):
 
 
 class FitResidualWorkload(FitWorkload):
-    """One step = one rti_fit_shared_residual call: coefficients + per-pixel RMS residuals + per-workgroup
-    residual energy in one pass over the stack (fp64 accumulation)."""
+    """One step = one rti_fit_shared_residual_svd call (what rti.fit_with_residual runs): coefficients +
+    per-pixel RMS residuals + per-workgroup residual energy in one pass over the stack (fp64 accumulation of
+    Uᵀ I and ‖I‖², the reference's SVD solve)."""
 
     def __init__(self, args, cfg, ctx):
         import torch
@@ -321,17 +322,17 @@ class FitResidualWorkload(FitWorkload):
         rti, L = self.rti, self.rti._lib
         k, N, C, P = self.k, self.N, self.C, self.P
         dev = ctx.dev
-        self.ginv = rti.gram_inverse(self.lu, self.lv, self.basis)
+        U, Wf = rti.lsq_factors(self.lu, self.lv, self.basis)
         self.A64 = rti.design_matrix(self.lu, self.lv, self.basis)
-        self.A_dev = torch.as_tensor(self.A64, device=dev).contiguous()
-        self.ginv_dev = torch.as_tensor(self.ginv, device=dev).contiguous()
+        self.A_dev = torch.as_tensor(U, device=dev).contiguous()
+        self.ginv_dev = torch.as_tensor(Wf, device=dev).contiguous()
         self.res = torch.empty((C, P), dtype=torch.float32, device=dev)
         nb = int(L.lib().rti_fit_shared_residual_blocks(P))
         self.partial = torch.zeros((C, nb), dtype=torch.float64, device=dev)
         self.alg_bytes += 4.0 * P * C  # + fp32 residual map
         self.metric = f"Mpix*lights/sec {self.desc}"
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        fn = L.lib().rti_fit_shared_residual
+        fn = L.lib().rti_fit_shared_residual_svd
         cargs = (ctypes.c_void_p(self.A_dev.data_ptr()), ctypes.c_void_p(self.ginv_dev.data_ptr()), k, N,
                  ctypes.c_void_p(self.I.data_ptr()), rti.api._IN_DTYPES[self.I.dtype], P, C, P, N * P,
                  ctypes.c_void_p(self.coef.data_ptr()), rti.api._layout_id(args.layout), P * k,
@@ -340,7 +341,7 @@ class FitResidualWorkload(FitWorkload):
         def step(i):
             st = fn(*cargs)
             if st:
-                L.check(st, "rti_fit_shared_residual")
+                L.check(st, "rti_fit_shared_residual_svd")
 
         self.step = step
         step(0)

@@ -116,6 +116,12 @@ int rti_basis_eval(int basis, const double* lu, const double* lv, int E, double*
  * design and SVD as rti_pinv (so pinv = ginv·Aᵀ; rcond as there), the operator with which
  * rti_fit_shared_residual turns Aᵀ I into coefficients (analysis.py:293-298). */
 int rti_gram_inverse(int basis, const float* lu, const float* lv, int n, double rcond, double* ginv);
+/* rti_lsq_factors: the thin SVD A = U Σ Vᵀ of the same shared design (same Jacobi SVD, rcond as in
+ * rti_pinv) split as the reference's solve splits it (analysis.py:295-298: c = uᵀL, w = c/s, a = vᵀw):
+ * U[n][k] = the orthonormal left singular vectors, W[k][k] = V Σ⁻¹ (W[i][m] = v_im / σ_m), so that
+ * pinv = W·Uᵀ.  A truncated σ_m zeroes column m of both; σ_m = 0 without rcond leaves NaN in
+ * column m (0·inf), the reference's division by a zero singular value.  Host fp64. */
+int rti_lsq_factors(int basis, const float* lu, const float* lv, int n, double rcond, double* U, double* W);
 
 /* ---- device: shared-direction fit (the north_star hot path) ------------------------
  * Replaces interpolate_intensities' per-pixel loop + _interpolate_PTM's solve
@@ -164,6 +170,16 @@ int rti_fit_shared_residual(const double* A, const double* ginv, int k, int N, c
                             int64_t P, int C, int64_t light_stride, int64_t channel_stride,
                             float* coef, int coef_layout, int64_t coef_channel_stride,
                             float* res, double* partial, int kernel, rti_stream_t stream);
+/* The same one-pass fit with the reference's SVD solve instead of the Gram form (analysis.py:295-298):
+ *   y = Uᵀ I[c][·][p], q = ‖I[c][·][p]‖²      (fp64),  coef = W · y,  ss = q − yᵀ y
+ * U: device fp64 [N][k], W: device fp64 [k][k] (rti_lsq_factors).  Never forms AᵀA, so coefficients
+ * keep cond(A)·1e-16 relative accuracy (the Gram form: cond(A)²·1e-16) — what the reference's SVD
+ * returns for ill-conditioned light sets.  Every other argument, the traffic and the speed as
+ * rti_fit_shared_residual; this is the form rti.fit_with_residual uses. */
+int rti_fit_shared_residual_svd(const double* U, const double* W, int k, int N, const void* I, int in_dtype,
+                                int64_t P, int C, int64_t light_stride, int64_t channel_stride,
+                                float* coef, int coef_layout, int64_t coef_channel_stride,
+                                float* res, double* partial, int kernel, rti_stream_t stream);
 
 /* ---- device: per-pixel PTM fit, light vectors generated in-kernel ------------------
  * Fuses compute_intensities' light vectors (analysis.py:221-231) into the

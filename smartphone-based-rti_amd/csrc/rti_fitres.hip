@@ -11,6 +11,17 @@
 //     ss        = q − coefᵀ b = ‖I − A·coef‖²  (the least-squares residual energy)
 //     res[c][p] = sqrt(ss / N),  partial[c][blk] = Σ ss over the workgroup (fp64)
 //
+// or, with the thin SVD factors A = U Σ Vᵀ instead of (A, G⁺) (rti_fit_shared_residual_svd, the
+// reference's own solve, analysis.py:295-298: c = uᵀL, w = c/s, a = vᵀw):
+//
+//     y         = Uᵀ I                     (k fp64 accumulators per pixel, U orthonormal [N][k])
+//     coef      = (V Σ⁻¹) y
+//     ss        = q − yᵀ y                 (‖I‖² minus the energy of its projection on range(A))
+//
+// The SVD form never forms AᵀA: its coefficients carry cond(A)·1e-16 relative error like the
+// reference's SVD, where the Gram form's carry cond(A)²·1e-16 (near-collinear lights,
+// tests/golden/ptm_edge.npz: 2.7e-7 vs 1e-15 of max|c| at cond(A) = 1.1e8).
+//
 // fp32 × fp32 products are exact in fp64, so b and q carry ~1e-16 relative error and the
 // subtraction q − coefᵀb (≈4e6 − 4e6 → ≈400 at N = 100, 8-bit data) keeps ~1e-9 absolute:
 // the one-pass identity that cancels catastrophically in fp32 (rti_residual.hip) is exact enough
@@ -57,7 +68,7 @@ template <int K, int VEC>
 constexpr bool fr_stage() { return VEC == 4 && (VEC * K) % 4 == 0 && K <= 9; }
 
 template <int K, int VEC, int NC, int U, typename T, int LAYOUT, bool TAIL>
-__device__ __forceinline__ double fitres_body(const double* __restrict__ A, const double* __restrict__ G, int N,
+__device__ __forceinline__ double fitres_body(const double* __restrict__ A, const double* __restrict__ G, int N, bool orth,
                                               const T* __restrict__ src, int64_t P, int64_t pe, int64_t lstride,
                                               float* __restrict__ dst, float* __restrict__ res,
                                               int64_t wave_base, int lane, float* lds_wave) {
@@ -131,10 +142,10 @@ __device__ __forceinline__ double fitres_body(const double* __restrict__ A, cons
         double ci = 0.0;
 #pragma unroll
         for (int l = 0; l < K; ++l) ci = fma(G[i * K + l], b[l][j], ci);
-        s = fma(-ci, b[i][j], s);
+        s = fma(orth ? -b[i][j] : -ci, b[i][j], s);
         o[v * K + i] = (float)ci;
       }
-      s = s > 0.0 ? s : 0.0;  // rounding can leave an exact fit a few ulps below zero
+      s = s < 0.0 ? 0.0 : s;  // rounding can leave an exact fit a few ulps below zero; NaN passes
       r[v] = (float)sqrt(s * invN);
       if (ok[c]) ss_sum += s;
     }
@@ -188,7 +199,7 @@ __device__ __forceinline__ double fitres_body(const double* __restrict__ A, cons
 
 template <int K, int VEC, int NC, int U, typename T, int LAYOUT>
 __global__ void __launch_bounds__(FR_THREADS)
-fit_shared_residual_k(const double* __restrict__ A, const double* __restrict__ G, int N, const T* __restrict__ I,
+fit_shared_residual_k(const double* __restrict__ A, const double* __restrict__ G, int N, int orth, const T* __restrict__ I,
                       int64_t P, int64_t pb, int64_t pe, int64_t lstride, int64_t cstride, float* __restrict__ coef,
                       int64_t ocstride, float* __restrict__ res, double* __restrict__ partial, int64_t pstride) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
@@ -205,10 +216,10 @@ fit_shared_residual_k(const double* __restrict__ A, const double* __restrict__ G
   double mine = 0.0;
   if (wave_base < pe) {  // wave-uniform; idle waves of the last workgroup still join the reduction
     if (wave_base + (int64_t)(64 * VEC * NC) <= pe)
-      mine = fitres_body<K, VEC, NC, U, T, LAYOUT, false>(A, G, N, src, P, pe, lstride, dst, rc, wave_base, lane,
+      mine = fitres_body<K, VEC, NC, U, T, LAYOUT, false>(A, G, N, orth != 0, src, P, pe, lstride, dst, rc, wave_base, lane,
                                                           lds_wave);
     else
-      mine = fitres_body<K, VEC, NC, U, T, LAYOUT, true>(A, G, N, src, P, pe, lstride, dst, rc, wave_base, lane,
+      mine = fitres_body<K, VEC, NC, U, T, LAYOUT, true>(A, G, N, orth != 0, src, P, pe, lstride, dst, rc, wave_base, lane,
                                                          lds_wave);
   }
   if (partial) {
@@ -236,6 +247,7 @@ struct FrArgs {
   float* res;
   double* partial;
   int nc;
+  int orth = 0;  // (A, G) = (U, V Σ⁻¹): ss = q − yᵀy
   hipStream_t s;
   int64_t pb = 0, pe = 0;  // this launch's pixel range [pb, pe) (pe 0 = P); pb a multiple of the workgroup span
 };
@@ -248,7 +260,7 @@ int launch_fr_t(const FrArgs& a) {
   const size_t lds =
       (LAYOUT == RTI_COEF_PIXEL_MAJOR && fr_stage<K, VEC>()) ? (size_t)FR_THREADS * VEC * K * sizeof(float) : 0;
   hipLaunchKernelGGL((fit_shared_residual_k<K, VEC, NC, U, T, LAYOUT>), grid, dim3(FR_THREADS), lds, a.s, a.A, a.G,
-                     a.N, static_cast<const T*>(a.I), a.P, a.pb, pe, a.lstride, a.cstride, a.coef, a.ocstride, a.res, a.partial,
+                     a.N, a.orth, static_cast<const T*>(a.I), a.P, a.pb, pe, a.lstride, a.cstride, a.coef, a.ocstride, a.res, a.partial,
                      (int64_t)grid_1d(a.P, FR_THREADS));
   return check_launch("rti_fit_shared_residual");
 }
@@ -302,10 +314,11 @@ extern "C" int64_t rti_fit_shared_residual_blocks(int64_t P) {
   return (int64_t)grid_1d(P, FR_THREADS);  // bounds every (VEC, NC) grid of the launch
 }
 
-extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int k, int N, const void* I, int in_dtype,
-                                       int64_t P, int C, int64_t light_stride, int64_t channel_stride, float* coef,
-                                       int coef_layout, int64_t coef_channel_stride, float* res, double* partial,
-                                       int kernel, rti_stream_t stream) {
+namespace {
+int fit_shared_residual_impl(bool orth, const double* A, const double* ginv, int k, int N, const void* I, int in_dtype,
+                             int64_t P, int C, int64_t light_stride, int64_t channel_stride, float* coef,
+                             int coef_layout, int64_t coef_channel_stride, float* res, double* partial, int kernel,
+                             rti_stream_t stream) {
   if (!A || !ginv || !I || !coef) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: null pointer");
   if (N <= 0 || P <= 0 || C <= 0 || C > 65535) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: bad N/P/C");
   if (N < k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: N=%d < k=%d", N, k);
@@ -329,6 +342,7 @@ extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int 
   a.ocstride = coef_channel_stride ? coef_channel_stride : P * k;
   a.res = res;
   a.partial = partial;
+  a.orth = orth ? 1 : 0;
   a.s = (hipStream_t)stream;
   if (a.lstride < P) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: light_stride < P");
   if (C > 1 && a.cstride < (int64_t)N * a.lstride)
@@ -404,4 +418,22 @@ extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int 
     }
   }
   return RTI_OK;
+}
+}  // namespace
+
+extern "C" int rti_fit_shared_residual(const double* A, const double* ginv, int k, int N, const void* I, int in_dtype,
+                                       int64_t P, int C, int64_t light_stride, int64_t channel_stride, float* coef,
+                                       int coef_layout, int64_t coef_channel_stride, float* res, double* partial,
+                                       int kernel, rti_stream_t stream) {
+  return fit_shared_residual_impl(false, A, ginv, k, N, I, in_dtype, P, C, light_stride, channel_stride, coef,
+                                  coef_layout, coef_channel_stride, res, partial, kernel, stream);
+}
+
+extern "C" int rti_fit_shared_residual_svd(const double* U, const double* W, int k, int N, const void* I,
+                                           int in_dtype, int64_t P, int C, int64_t light_stride,
+                                           int64_t channel_stride, float* coef, int coef_layout,
+                                           int64_t coef_channel_stride, float* res, double* partial, int kernel,
+                                           rti_stream_t stream) {
+  return fit_shared_residual_impl(true, U, W, k, N, I, in_dtype, P, C, light_stride, channel_stride, coef,
+                                  coef_layout, coef_channel_stride, res, partial, kernel, stream);
 }

@@ -59,8 +59,12 @@ static void design_row(int basis, float lu, float lv, double* row) {
 
 // One-sided (Hestenes) Jacobi SVD of A[n][k] (row-major, n >= k) and
 // pinv[k][n] = V Σ⁻¹ Uᵀ = Σ_m v_m (A v_m)ᵀ / σ_m²; optionally the Gram (pseudo-)inverse
-// ginv[k][k] = (AᵀA)⁺ = V Σ⁻² Vᵀ, so that pinv = ginv · Aᵀ.
-static void jacobi_pinv(const double* A, int n, int k, double rcond, double* pinv, double* ginv = nullptr) {
+// ginv[k][k] = (AᵀA)⁺ = V Σ⁻² Vᵀ, so that pinv = ginv · Aᵀ, and the thin SVD factors themselves
+// (Uo[n][k] = A v_m / σ_m, the orthonormal left singular vectors; Wo[k][k] = V Σ⁻¹), the two halves of
+// analysis.py:295-298 (c = uᵀL, w = c/s, a = vᵀw).  A truncated σ (rcond) zeroes its column of Uo and Wo;
+// σ = 0 without rcond gives 0·inf = NaN entries, the reference's division by a zero singular value.
+static void jacobi_pinv(const double* A, int n, int k, double rcond, double* pinv, double* ginv = nullptr,
+                        double* Uo = nullptr, double* Wo = nullptr) {
   std::vector<double> U(A, A + (size_t)n * k);  // column j = U[i*k + j]; becomes U·Σ
   std::vector<double> V((size_t)k * k, 0.0);
   for (int j = 0; j < k; ++j) V[(size_t)j * k + j] = 1.0;
@@ -137,6 +141,12 @@ static void jacobi_pinv(const double* A, int n, int k, double rcond, double* pin
         }
         ginv[(size_t)j * k + l] = acc;
       }
+  if (Uo && Wo)
+    for (int m = 0; m < k; ++m) {
+      const double is = inv2[m] == 0.0 ? 0.0 : 1.0 / std::sqrt(sig2[m]);
+      for (int i = 0; i < n; ++i) Uo[(size_t)i * k + m] = U[(size_t)i * k + m] * is;
+      for (int j = 0; j < k; ++j) Wo[(size_t)j * k + m] = V[(size_t)j * k + m] * is;
+    }
 }
 
 // LU factorisation with partial pivoting (LAPACK getrf semantics), in place, row-major n×n.
@@ -248,6 +258,19 @@ int rti_gram_inverse(int basis, const float* lu, const float* lv, int n, double 
   std::vector<double> A((size_t)n * k);
   for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], &A[(size_t)i * k]);
   jacobi_pinv(A.data(), n, k, rcond, nullptr, ginv);
+  return RTI_OK;
+}
+
+int rti_lsq_factors(int basis, const float* lu, const float* lv, int n, double rcond, double* U, double* W) {
+  const int k = basis_terms(basis);
+  if (k < 0) return fail(RTI_ERR_BAD_ARG, "rti_lsq_factors: unknown basis %d", basis);
+  if (!lu || !lv || !U || !W || n <= 0) return fail(RTI_ERR_BAD_ARG, "rti_lsq_factors: null pointer or n <= 0");
+  if (n < k)
+    return fail(RTI_ERR_BAD_ARG, "rti_lsq_factors: %d lights < %d basis terms (shapes not aligned, analysis.py:298)", n,
+                k);
+  std::vector<double> A((size_t)n * k);
+  for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], &A[(size_t)i * k]);
+  jacobi_pinv(A.data(), n, k, rcond, nullptr, nullptr, U, W);
   return RTI_OK;
 }
 

@@ -8,9 +8,12 @@
 // (as the reference's float32 monomials), accumulates the 6×6 normal
 // equations AᵀA, Aᵀb in fp64 and solves them by Cholesky in fp64.  For a
 // full-rank A that is the same least-squares solution the SVD returns (the
-// fp64 normal equations lose cond(A)²·1e-16, far below the 1e-4 parity
-// tolerance for cond(A) < 1e3); a rank-deficient A gives NaN coefficients, as
-// the reference's division by a zero singular value does.
+// fp64 normal equations lose cond(A)²·1e-16); a pixel whose Cholesky pivots
+// show an ill-conditioned A (ne_solve) is marked and re-solved by a second,
+// refine launch (qr_refine_*) with a streaming fp64 Givens QR of A itself
+// (qr_solve), which loses cond(A)·1e-16 like the reference's SVD; a
+// rank-deficient A gives NaN coefficients, as the reference's division by a
+// zero singular value does.
 //
 //  * fit_perpixel_cam : directions generated in-kernel from cams[N][3]
 //    (light-major, coalesced intensity planes; no lx/ly traffic at all).
@@ -65,37 +68,75 @@ __device__ __forceinline__ void ne_add(Normal6& ne, float lu, float lv, double L
 
 __device__ __forceinline__ void ne_finish(Normal6& ne, int N) { ne.m[tri(5, 5)] = (double)N; }
 
-// compute_intensities' direction l = d / ‖d‖ (analysis.py:228-229), components rounded to
-// fp32 (:230-231).  1/‖d‖ is the v_rsq_f64 seed refined by two Newton steps (a few fp64
-// ulps), so the fp32 components equal the correctly rounded quotient except when the fp64
-// value lies within those few ulps of an fp32 rounding midpoint (≈1e-8 of inputs; the
-// fit then moves by ~1e-8 relative).  15 VALU ops instead of sqrt + two IEEE divides.
-__device__ __forceinline__ void light_dir_fast(double dx, double dy, double dz, float& lu, float& lv) {
-  const double d2 = fma(dx, dx, fma(dy, dy, dz * dz));
-  double y = __builtin_amdgcn_rsq(d2);
-  const double h = 0.5 * d2;
+// compute_intensities' direction l = d / ‖d‖ (analysis.py:228-229), components rounded to fp32
+// (:230-231), BIT-EXACT with the reference's arrays at almost the cost of an rsq: the reference rounds
+// s = (dx² + dy²) + dz² op by op, n = sqrt(s) and q = dx / n correctly (IEEE fp64), then q to fp32.
+// Here s is formed the same way (no contraction), 1/√s is the v_rsq_f64 seed refined by two Newton
+// steps, and q̃ = dx·(1/√s) lies within a few fp64 ulps of q.  fp32 rounding looks only at the low 29
+// bits of q's fp64 significand, so fp32(q̃) == fp32(q) unless q̃ lies within those few ulps of an fp32
+// rounding midpoint (low 29 bits = 2^28) — then (≈1 in 4·10⁶ lights) the pixel is marked and the
+// refine pass recomputes its light vectors with the IEEE sqrt and divide of rti_light_dirs.  Pinned by
+// tests/golden/ptm_perpixel_32x32_N50.npz through
+// rti_fit_perpixel_cam (test_gpu_perpixel_relight.py).
+__device__ __forceinline__ bool near_f32_midpoint(double q) {
+  constexpr uint32_t MARGIN = 64;  // fp64 ulps: the Newton-refined quotient is within ~4 of IEEE's
+  const uint32_t lo = (uint32_t)__double_as_longlong(q) & 0x1FFFFFFFu;
+  return lo - (0x10000000u - MARGIN) < 2 * MARGIN;
+}
+
+// The fast form: `ambiguous` is set when the lane's fp32 rounding could differ from the reference's
+// (a quotient near an fp32 midpoint, or s tiny/non-finite); the fit then marks the pixel and the refine
+// pass (light_dir_exact) redoes it, so the hot loop carries no sqrt/divide code.
+__device__ __forceinline__ void light_dir_fast(double dx, double dy, double dz, float& lu, float& lv,
+                                               bool& ambiguous) {
+#pragma clang fp contract(off)
+  const double s = dx * dx + dy * dy + dz * dz;  // (dx² + dy²) + dz², each op rounded
+  double y = __builtin_amdgcn_rsq(s);
+  const double h = 0.5 * s;
   y = fma(y, fma(-h * y, y, 0.5), y);
   y = fma(y, fma(-h * y, y, 0.5), y);
-  lu = (float)(dx * y);
-  lv = (float)(dy * y);
+  const double qx = dx * y, qy = dy * y;
+  // fp32 subnormal results round on more bits: |q| below 2^-120 (and not 0) is also ambiguous
+  ambiguous = ambiguous || near_f32_midpoint(qx) || near_f32_midpoint(qy) || !(s > 0x1p-900) ||
+              (fabs(qx) < 0x1p-120 && qx != 0.0) || (fabs(qy) < 0x1p-120 && qy != 0.0);
+  lu = (float)qx;
+  lv = (float)qy;
+}
+
+__device__ __forceinline__ void light_dir_exact(double dx, double dy, double dz, float& lu, float& lv) {
+#pragma clang fp contract(off)
+  bool amb = false;
+  light_dir_fast(dx, dy, dz, lu, lv, amb);
+  if (amb) {
+    const double n = sqrt(dx * dx + dy * dy + dz * dz);
+    lu = (float)(dx / n);
+    lv = (float)(dy / n);
+  }
 }
 
 // Cholesky solve of (AᵀA) a = Aᵀb.  rcond < 0: singular only at a non-positive
 // pivot (reference semantics); rcond >= 0: pivots <= rcond²·max(diag) count
-// as singular.  Singular -> all-NaN coefficients.
-__device__ __forceinline__ void ne_solve(const Normal6& ne, double rcond, double (&a)[6]) {
+// as singular.  Singular -> all-NaN coefficients.  Returns true when the system is
+// ill-conditioned for the normal equations: a pivot kept less than ILL_RATIO of its
+// column's squared norm (the scaled cond(A)² ≳ 1/ILL_RATIO, where the normal equations
+// lose cond(A)²·1e-16 against the reference's SVD) — the caller then re-solves the pixel by
+// Givens QR of A itself (qr_solve), which loses only cond(A)·1e-16 like the SVD.
+constexpr double ILL_RATIO = 1e-6;
+
+__device__ __forceinline__ bool ne_solve(const Normal6& ne, double rcond, double (&a)[6]) {
   double L[6][6];
   double dmax = 0.0;
 #pragma unroll
   for (int i = 0; i < 6; ++i) dmax = fmax(dmax, ne.m[tri(i, i)]);
   const double thr = rcond < 0.0 ? 0.0 : rcond * rcond * dmax;
-  bool ok = true;
+  bool ok = true, ill = false;
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     double d = ne.m[tri(j, j)];
 #pragma unroll
     for (int p = 0; p < j; ++p) d -= L[j][p] * L[j][p];
     ok = ok && (d > thr);
+    ill = ill || !(d > ILL_RATIO * ne.m[tri(j, j)]);
     const double ljj = sqrt(d > 0.0 ? d : 1.0);
     L[j][j] = ljj;
     const double inv = 1.0 / ljj;
@@ -126,6 +167,73 @@ __device__ __forceinline__ void ne_solve(const Normal6& ne, double rcond, double
 #pragma unroll
     for (int i = 0; i < 6; ++i) a[i] = __builtin_nan("");
   }
+  return ok && ill;  // an exactly singular system stays NaN (the reference's zero singular value)
+}
+
+// Least squares by Givens QR of [A | L] streamed row by row in fp64 (R upper 6×6 packed, z = QᵀL):
+// backward stable in A itself, so the solution carries cond(A)·1e-16 relative error — the accuracy of
+// the reference's SVD (analysis.py:295-298) for the ill-conditioned light sets the normal equations
+// cannot take (tests/golden/ptm_edge.npz near-collinear lights, cond(A) = 1.1e8).  `row(n, r, L)`
+// yields light n's PTM row and intensity.  Singular semantics as ne_solve: AᵀA = RᵀR, so a pivot
+// R_jj² <= rcond²·max diag(AᵀA) (rcond >= 0) or R_jj = 0 gives NaN coefficients.
+template <typename Row>
+__device__ __forceinline__ void qr_solve(int N, double rcond, Row row, double (&a)[6]) {
+  double R[21], z[6], cn[6];
+#pragma unroll
+  for (int i = 0; i < 21; ++i) R[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) z[i] = cn[i] = 0.0;
+  for (int n = 0; n < N; ++n) {
+    double x[6], l;
+    row(n, x, l);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) cn[i] = fma(x[i], x[i], cn[i]);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const double xj = x[j];
+      if (xj == 0.0) continue;
+      const double rjj = R[tri(j, j)];
+      const double m = fmax(fabs(rjj), fabs(xj));  // scaled hypot: no overflow/underflow
+      const double h = m * sqrt((rjj / m) * (rjj / m) + (xj / m) * (xj / m));
+      const double c = rjj / h, sn = xj / h;
+      R[tri(j, j)] = h;
+#pragma unroll
+      for (int k = j + 1; k < 6; ++k) {
+        const double t = R[tri(j, k)];
+        R[tri(j, k)] = fma(c, t, sn * x[k]);
+        x[k] = fma(-sn, t, c * x[k]);
+      }
+      const double t = z[j];
+      z[j] = fma(c, t, sn * l);
+      l = fma(-sn, t, c * l);
+    }
+  }
+  double cmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) cmax = fmax(cmax, cn[i]);
+  const double thr = rcond < 0.0 ? 0.0 : rcond * sqrt(cmax);
+  bool ok = true;
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    ok = ok && (R[tri(i, i)] > thr);
+    double s = z[i];
+#pragma unroll
+    for (int p = i + 1; p < 6; ++p) s -= R[tri(i, p)] * a[p];
+    a[i] = s / R[tri(i, i)];
+  }
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a[i] = __builtin_nan("");
+  }
+}
+
+__device__ __forceinline__ void ptm_row_d(float lu, float lv, double (&r)[6]) {
+  r[0] = (double)(lu * lu);
+  r[1] = (double)(lv * lv);
+  r[2] = (double)(lu * lv);
+  r[3] = (double)lu;
+  r[4] = (double)lv;
+  r[5] = 1.0;
 }
 
 template <typename TC, int LAYOUT>
@@ -137,6 +245,44 @@ __device__ __forceinline__ void store_coef(TC* __restrict__ coef, int64_t P, int
     else
       coef[p * 6 + i] = (TC)a[i];
   }
+}
+
+// A pixel the normal equations cannot take leaves this signalling-NaN bit pattern in its first
+// coefficient for the refine pass (qr_refine_*), which re-solves exactly those pixels by Givens QR.
+// No arithmetic produces it (results are quiet NaNs), and the refine pass overwrites every instance.
+template <typename TC>
+struct QrMark;
+template <>
+struct QrMark<double> {
+  using U = unsigned long long;
+  static constexpr U bits = 0x7FF0515249514D4Bull;
+};
+template <>
+struct QrMark<float> {
+  using U = unsigned int;
+  static constexpr U bits = 0x7FA51A11u;
+};
+
+template <typename TC, int LAYOUT>
+__device__ __forceinline__ TC* coef0(TC* coef, int64_t P, int64_t p) {
+  (void)P;
+  return LAYOUT == RTI_COEF_PLANAR ? coef + p : coef + p * 6;
+}
+
+template <typename TC, int LAYOUT>
+__device__ __forceinline__ void solve_store(const Normal6& ne, double rcond, TC* __restrict__ coef, int64_t P,
+                                            int64_t p, bool redo = false) {
+  double a[6];
+  const bool ill = ne_solve(ne, rcond, a) || redo;
+  store_coef<TC, LAYOUT>(coef, P, p, a);
+  if (__builtin_expect(ill, 0))
+    *reinterpret_cast<typename QrMark<TC>::U*>(coef0<TC, LAYOUT>(coef, P, p)) = QrMark<TC>::bits;
+}
+
+template <typename TC, int LAYOUT>
+__device__ __forceinline__ bool qr_marked(const TC* coef, int64_t P, int64_t p) {
+  return *reinterpret_cast<const typename QrMark<TC>::U*>(coef0<TC, LAYOUT>(const_cast<TC*>(coef), P, p)) ==
+         QrMark<TC>::bits;
 }
 
 template <typename T, typename TC, int LAYOUT>
@@ -151,15 +297,37 @@ fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I
   Normal6 ne;
   ne_zero(ne);
   const T* __restrict__ src = I + p;
+  bool amb = false;
 #pragma unroll 4
   for (int n = 0; n < N; ++n) {
     float lu, lv;  // cams: wave-uniform -> scalar loads
-    light_dir_fast(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv);
+    light_dir_fast(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv, amb);
     ne_add(ne, lu, lv, ld_d(src + (int64_t)n * lstride));
   }
   ne_finish(ne, N);
+  solve_store<TC, LAYOUT>(ne, rcond, coef, P, p, amb);
+}
+
+// Refine pass of fit_perpixel_cam: the marked pixels (ill-conditioned, or a light vector the fast form
+// could not round with certainty) with exact light vectors and Givens QR (qr_solve).  A scan of
+// one coefficient per pixel when nothing is marked (8 B per pixel against the fit's 4·N).
+template <typename T, typename TC, int LAYOUT>
+__global__ void __launch_bounds__(256)
+qr_refine_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
+              double x0, double y0, double rcond, TC* __restrict__ coef) {
+  const int64_t P = (int64_t)H * W;
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P || !qr_marked<TC, LAYOUT>(coef, P, p)) return;
+  const double px = x0 + (double)(p % W);
+  const double py = y0 + (double)(p / W);
+  const T* __restrict__ src = I + p;
   double a[6];
-  ne_solve(ne, rcond, a);
+  qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
+    float lu, lv;
+    light_dir_exact(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv);
+    ptm_row_d(lu, lv, r);
+    L = ld_d(src + (int64_t)n * lstride);
+  }, a);
   store_coef<TC, LAYOUT>(coef, P, p, a);
 }
 
@@ -175,8 +343,21 @@ fit_perpixel_dirs(const float* __restrict__ lu, const float* __restrict__ lv, co
 #pragma unroll 4
   for (int n = 0; n < N; ++n) ne_add(ne, lu[base + n], lv[base + n], ld_d(I + base + n));
   ne_finish(ne, N);
+  solve_store<TC, LAYOUT>(ne, rcond, coef, P, p);
+}
+
+template <typename T, typename TC, int LAYOUT>
+__global__ void __launch_bounds__(256)
+qr_refine_dirs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N,
+               int64_t P, double rcond, TC* __restrict__ coef) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P || !qr_marked<TC, LAYOUT>(coef, P, p)) return;
+  const int64_t base = p * N;
   double a[6];
-  ne_solve(ne, rcond, a);
+  qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
+    ptm_row_d(lu[base + n], lv[base + n], r);
+    L = ld_d(I + base + n);
+  }, a);
   store_coef<TC, LAYOUT>(coef, P, p, a);
 }
 
@@ -207,6 +388,8 @@ void launch_cam(const double* cams, int N, const void* I, int H, int W, int64_t 
   const int64_t P = (int64_t)H * W;
   hipLaunchKernelGGL((fit_perpixel_cam<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N,
                      static_cast<const T*>(I), H, W, ls, x0, y0, rcond, static_cast<TC*>(coef));
+  hipLaunchKernelGGL((qr_refine_cam<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N,
+                     static_cast<const T*>(I), H, W, ls, x0, y0, rcond, static_cast<TC*>(coef));
 }
 
 template <typename T, typename TC>
@@ -231,6 +414,8 @@ template <typename T, typename TC, int LAYOUT>
 void launch_dirs(const float* lu, const float* lv, const void* I, int N, int64_t P, double rcond, void* coef,
                  hipStream_t s) {
   hipLaunchKernelGGL((fit_perpixel_dirs<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, lu, lv,
+                     static_cast<const T*>(I), N, P, rcond, static_cast<TC*>(coef));
+  hipLaunchKernelGGL((qr_refine_dirs<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, lu, lv,
                      static_cast<const T*>(I), N, P, rcond, static_cast<TC*>(coef));
 }
 

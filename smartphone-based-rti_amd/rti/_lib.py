@@ -80,6 +80,7 @@ SIGNATURES = {
     "rti_pinv": (_c_int, [_c_int, _c_float_p, _c_float_p, _c_int, _c_double, _c_double_p]),
     "rti_basis_eval": (_c_int, [_c_int, _c_double_p, _c_double_p, _c_int, _c_double_p]),
     "rti_gram_inverse": (_c_int, [_c_int, _c_float_p, _c_float_p, _c_int, _c_double, _c_double_p]),
+    "rti_lsq_factors": (_c_int, [_c_int, _c_float_p, _c_float_p, _c_int, _c_double, _c_double_p, _c_double_p]),
     "rti_fit_shared": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_int, _c_i64, _c_int, _c_i64, _c_i64,
                                 _c_void_p, _c_int, _c_i64, _c_int, _c_void_p]),
     "rti_fit_residual_blocks": (_c_i64, [_c_i64]),
@@ -89,6 +90,9 @@ SIGNATURES = {
     "rti_fit_shared_residual": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_int, _c_i64, _c_int,
                                          _c_i64, _c_i64, _c_void_p, _c_int, _c_i64, _c_void_p, _c_void_p, _c_int,
                                          _c_void_p]),
+    "rti_fit_shared_residual_svd": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_int, _c_i64,
+                                             _c_int, _c_i64, _c_i64, _c_void_p, _c_int, _c_i64, _c_void_p, _c_void_p,
+                                             _c_int, _c_void_p]),
     "rti_fit_perpixel_cam": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_int, _c_int, _c_int, _c_i64, _c_double,
                                       _c_double, _c_double, _c_void_p, _c_int, _c_int, _c_void_p]),
     "rti_fit_perpixel_dirs": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_i64, _c_double,

@@ -100,6 +100,22 @@ def gram_inverse(lu, lv, basis="ptm", rcond=None):
     return out
 
 
+def lsq_factors(lu, lv, basis="ptm", rcond=None):
+    """Host fp64 thin-SVD factors ``(U [N, k], W [k, k])`` of the shared design, split as the
+    reference's solve is (analysis.py:295-298: ``c = uᵀL; w = c/s; a = vᵀw``): U = the orthonormal
+    left singular vectors, W = V Σ⁻¹, so pinv = W·Uᵀ (rcond as ``pinv``)."""
+    lu, lv = _f32_host(lu, "lu"), _f32_host(lv, "lv")
+    if lu.size != lv.size:
+        raise ValueError("lu and lv differ in length")
+    b = basis_id(basis)
+    k = basis_terms(b)
+    U = np.empty((lu.size, k), dtype=np.float64)
+    W = np.empty((k, k), dtype=np.float64)
+    rc = -1.0 if rcond is None else float(rcond)
+    L.check(L.lib().rti_lsq_factors(b, _fptr(lu), _fptr(lv), lu.size, rc, _dptr(U), _dptr(W)), "rti_lsq_factors")
+    return U, W
+
+
 def basis_eval(lu, lv, basis="ptm"):
     """Host fp64 basis values [E, k] at (lu, lv)."""
     lu = np.ascontiguousarray(np.asarray(lu, np.float64).ravel())
@@ -296,15 +312,32 @@ def _stack_shape(I):
     return C, N, P, spatial
 
 
+def fit_shared_residual_into(U_dev, W_dev, I3, coef, res, partial, *, k, layout="pixel", chunks=0):
+    """Launch ``rti_fit_shared_residual_svd`` on preallocated tensors (no allocation, graph-capturable).
+
+    U_dev fp64 [N, k], W_dev fp64 [k, k] (``lsq_factors``), I3 CUDA [C, N, P] light-major, coef fp32
+    [C, P, k] / [C, k, P], res fp32 [C, P] (or None), partial fp64 [C, rti_fit_shared_residual_blocks(P)]
+    zeroed (or None)."""
+    C, N, P = I3.shape
+    cl = _layout_id(layout)
+    st = L.lib().rti_fit_shared_residual_svd(_vp(U_dev), _vp(W_dev), k, N, _vp(I3), _IN_DTYPES[I3.dtype], P, C, P,
+                                             N * P, _vp(coef), cl, P * k, None if res is None else _vp(res),
+                                             None if partial is None else _vp(partial),
+                                             int(chunks) << L.RTI_KERNEL_CHUNKS_SHIFT, _stream_of(I3))
+    L.check(st, "rti_fit_shared_residual_svd")
+
+
 def fit_with_residual(I, lu, lv, basis="ptm", rcond=None, *, layout="pixel", chunks=0):
     """Shared-direction fit AND per-pixel residuals in ONE pass over the stack
-    (``rti_fit_shared_residual``; fp64 accumulation of Aᵀ I and ‖I‖², coefficients = (AᵀA)⁺ Aᵀ I).
+    (``rti_fit_shared_residual_svd``: the reference's SVD solve, analysis.py:295-298, per pixel —
+    y = Uᵀ I and ‖I‖² accumulated in fp64, coefficients = V Σ⁻¹ y, residual energy ‖I‖² − ‖y‖²).
 
     I: CUDA [N, P], [N, H, W] or [C, N, H, W] (light-major, fp32/u8/int32).  Returns
     ``(coef, res, rms)``: coef fp32 as ``fit`` returns it (layout), res fp32 with I's spatial shape
     (leading C for 4-D stacks) = sqrt(Σ_n (I_n − A_n·coef)² / N) for the least-squares solution, and
     rms fp64 [C] (0-d for 2/3-D stacks) = the RMS residual over all pixels, summed from per-workgroup
-    wavefront reductions."""
+    wavefront reductions.  An exactly rank-deficient light set (rcond=None) gives NaN coefficients AND
+    NaN residuals, like the reference's division by a zero singular value."""
     _require_cuda(I, "I")
     if I.dtype not in _IN_DTYPES:
         raise ValueError(f"I dtype {I.dtype} unsupported (float32, uint8 or int32)")
@@ -314,20 +347,17 @@ def fit_with_residual(I, lu, lv, basis="ptm", rcond=None, *, layout="pixel", chu
     C, N, P, spatial = _stack_shape(I)
     if N < k:
         raise ValueError(f"shapes not aligned: {N} lights < {k} basis terms (analysis.py:298)")
-    A = design_matrix(lu, lv, b)
-    if A.shape[0] != N:
-        raise ValueError(f"{A.shape[0]} light directions for {N} intensity planes")
+    U, W = lsq_factors(lu, lv, b, rcond)
+    if U.shape[0] != N:
+        raise ValueError(f"{U.shape[0]} light directions for {N} intensity planes")
     dev = I.device
-    A_dev = torch.as_tensor(A, device=dev).contiguous()
-    G_dev = torch.as_tensor(gram_inverse(lu, lv, b, rcond), device=dev).contiguous()
+    U_dev = torch.as_tensor(U, device=dev).contiguous()
+    W_dev = torch.as_tensor(W, device=dev).contiguous()
     Ic = I.contiguous().reshape(C, N, P)
     coef = torch.empty((C, P, k) if cl == L.RTI_COEF_PIXEL_MAJOR else (C, k, P), dtype=torch.float32, device=dev)
     res = torch.empty((C, P), dtype=torch.float32, device=dev)
     partial = torch.zeros((C, int(L.lib().rti_fit_shared_residual_blocks(P))), dtype=torch.float64, device=dev)
-    st = L.lib().rti_fit_shared_residual(_vp(A_dev), _vp(G_dev), k, N, _vp(Ic), _IN_DTYPES[Ic.dtype], P, C, P, N * P,
-                                         _vp(coef), cl, P * k, _vp(res), _vp(partial),
-                                         int(chunks) << L.RTI_KERNEL_CHUNKS_SHIFT, _stream_of(I))
-    L.check(st, "rti_fit_shared_residual")
+    fit_shared_residual_into(U_dev, W_dev, Ic, coef, res, partial, k=k, layout=cl, chunks=chunks)
     rms = torch.sqrt(partial.sum(dim=1) / (P * N))
     coef = coef.reshape((C,) + spatial + (k,)) if cl == L.RTI_COEF_PIXEL_MAJOR else coef.reshape((C, k) + spatial)
     res = res.reshape((C,) + spatial)

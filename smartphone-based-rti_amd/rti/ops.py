@@ -1,4 +1,5 @@
-"""PyTorch custom ops over the C ABI: ``torch.ops.rti.fit_shared`` / ``fit_residual`` / ``relight``.
+"""PyTorch custom ops over the C ABI: ``torch.ops.rti.fit_shared`` / ``fit_shared_residual`` /
+``fit_residual`` / ``relight``.
 
 They let the fit and relight kernels sit inside torch programs (and
 ``torch.library`` fake-tensor tracing) while the compute stays in librti's
@@ -53,6 +54,52 @@ def _(pinv, I, planar=False, kernel=0):
     if I.dim() == 3:
         shape = (I.shape[0],) + shape
     return I.new_empty(shape, dtype=torch.float32)
+
+
+@torch.library.custom_op("rti::fit_shared_residual", mutates_args=())
+def fit_shared_residual(U: torch.Tensor, W: torch.Tensor, I: torch.Tensor, planar: bool = False,
+                        chunks: int = 0) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """The north_star fit with per-pixel residuals in ONE pass over the stack
+    (``rti_fit_shared_residual_svd``; the reference's solve, analysis.py:293-298, as y = Uᵀ I,
+    coef = W y with the thin SVD A = U Σ Vᵀ, W = V Σ⁻¹).
+
+    U fp64 [N, k], W fp64 [k, k] (``rti.lsq_factors``), I CUDA [N, P] or [C, N, P] (fp32/u8/int32) ->
+    ``(coef, res, partial)``: coef fp32 [C?, P, k] (or [C?, k, P] if planar), res fp32 [C?, P] =
+    sqrt(Σ_n (I_n − A_n·coef)² / N), partial fp64 [C?, rti_fit_shared_residual_blocks(P)] = each
+    workgroup's residual energy from wavefront reductions (sum / (P·N) = mean squared residual)."""
+    api._require_cuda(I, "I")
+    api._require_cuda(U, "U")
+    api._require_cuda(W, "W")
+    if U.dtype != torch.float64 or W.dtype != torch.float64:
+        raise ValueError("U and W must be float64 (rti.lsq_factors)")
+    _same_device(U=U, W=W, I=I)
+    _in_dtype(I)
+    I3 = I.contiguous() if I.dim() == 3 else I.contiguous().unsqueeze(0)
+    C, N, P = I3.shape
+    k = U.shape[1]
+    if U.shape[0] != N or W.shape != (k, k):
+        raise ValueError(f"U must be [{N}, k] and W [k, k]; got {tuple(U.shape)} and {tuple(W.shape)}")
+    if N < k:
+        raise ValueError(f"shapes not aligned: {N} lights < {k} basis terms (analysis.py:298)")
+    coef = torch.empty((C, k, P) if planar else (C, P, k), dtype=torch.float32, device=I.device)
+    res = torch.empty((C, P), dtype=torch.float32, device=I.device)
+    partial = torch.zeros((C, int(L.lib().rti_fit_shared_residual_blocks(P))), dtype=torch.float64, device=I.device)
+    api.fit_shared_residual_into(U.contiguous(), W.contiguous(), I3, coef, res, partial, k=k,
+                                 layout="planar" if planar else "pixel", chunks=chunks)
+    if I.dim() == 2:
+        return coef[0], res[0], partial[0]
+    return coef, res, partial
+
+
+@fit_shared_residual.register_fake
+def _(U, W, I, planar=False, chunks=0):
+    k = U.shape[1]
+    P = I.shape[-1]
+    lead = (I.shape[0],) if I.dim() == 3 else ()
+    nb = (P + 255) // 256  # rti_fit_shared_residual_blocks(P): one slot per 256-pixel workgroup span
+    return (I.new_empty(lead + ((k, P) if planar else (P, k)), dtype=torch.float32),
+            I.new_empty(lead + (P,), dtype=torch.float32),
+            I.new_empty(lead + (nb,), dtype=torch.float64))
 
 
 @torch.library.custom_op("rti::fit_residual", mutates_args=())

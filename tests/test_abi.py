@@ -121,3 +121,30 @@ def test_basis_eval_matches_oracle():
     assert np.abs(B - o.hsh_basis(lu, lv)).max() < 1e-13
     P = rti.basis_eval(lu, lv, "ptm")
     assert np.array_equal(P, np.stack([lu * lu, lv * lv, lu * lv, lu, lv, np.ones_like(lu)], -1))
+
+
+@pytest.mark.parametrize("case", ["exact6", "nearcollinear", "n200"])
+def test_lsq_factors_reproduce_reference_edge_goldens(case):
+    """rti_lsq_factors splits the reference's solve (analysis.py:295-298) as U (orthonormal) and
+    W = V Σ⁻¹: W·(Uᵀ I) gives the reference's own coefficients for its edge light sets, including the
+    near-collinear one (cond(A) = 1.1e8) where the normal equations lose 6.5e-3."""
+    e = golden("ptm_edge.npz")
+    U, W = rti.lsq_factors(e[f"{case}_lu"], e[f"{case}_lv"])
+    assert np.abs(U.T @ U - np.eye(6)).max() < 1e-14
+    ref = e[f"{case}_coef"]
+    got = W @ (U.T @ e[f"{case}_I"].astype(np.float64))
+    assert np.abs(got - ref).max() <= 1e-7 * np.abs(ref).max()
+    pv = rti.pinv(e[f"{case}_lu"], e[f"{case}_lv"])
+    assert np.abs(W @ U.T - pv).max() <= 1e-9 * np.abs(pv).max()
+
+
+def test_lsq_factors_rank_deficient_and_rcond():
+    e = golden("ptm_edge.npz")
+    U, W = rti.lsq_factors(e["singular_lu"], e["singular_lv"])
+    assert np.isnan(W @ (U.T @ e["singular_I"].astype(np.float64))).all()  # the reference's NaN
+    U, W = rti.lsq_factors(e["singular_lu"], e["singular_lv"], rcond=1e-10)
+    A = o.ptm_design(e["singular_lu"], e["singular_lv"])
+    ref = np.linalg.pinv(A, rcond=1e-10)
+    assert np.abs(W @ U.T - ref).max() < 1e-10 * np.abs(ref).max()
+    with pytest.raises(ValueError):
+        rti.lsq_factors(e["singular_lu"][:5], e["singular_lv"][:5])

@@ -1,7 +1,8 @@
-"""GPU parity of the one-pass fit + residual kernel (rti_fit_shared_residual) against the oracle
-and the reference's golden coefficients.
+"""GPU parity of the one-pass fit + residual kernel (rti_fit_shared_residual_svd, the form
+rti.fit_with_residual uses; the Gram form rti_fit_shared_residual in the generations test and
+test_gpu_edge_solvers.py) against the oracle and the reference's golden coefficients.
 
-The kernel accumulates Aᵀ I and ‖I‖² in fp64 (exact fp32×fp32 products), so its coefficients
+The kernel accumulates Uᵀ I and ‖I‖² in fp64, so its coefficients
 are held to 1e-6 of max_k |c_ref| per pixel (100× inside the SURVEY §8(c) 1e-4 bar) and its
 residuals — of the exact least-squares solution, compared with oracle.fit_residual evaluated on
 the fp64 reference coefficients — to |res − res_ref| <= 1e-4 + 1e-6·res_ref (intensity units)."""
@@ -149,12 +150,14 @@ def test_full_size_4k_n100(cuda):
     assert abs(float(rms) - expect) < 0.02 * expect
 
 
+@pytest.mark.parametrize("form", ["svd", "gram"])
 @pytest.mark.parametrize("layout", ["pixel", "planar"])
-def test_launch_generations_bit_identical(cuda, layout):
+def test_launch_generations_bit_identical(cuda, layout, form):
     """AUTO issues a large fit + residual call as consecutive launches over pixel ranges of whole
     workgroups (launch generations, rti_fitres.hip); coefficients, residuals and the per-workgroup
-    residual energies must equal RTI_KERNEL_ONE_LAUNCH's bit for bit (same chunks per lane here), over a
-    ragged pixel count and 2 channels, and match the fp64 oracle on sampled pixels."""
+    residual energies must equal RTI_KERNEL_ONE_LAUNCH's bit for bit, over a ragged pixel count and 2
+    channels, and match the fp64 oracle on sampled pixels.  Both runs pin 3 chunks per lane: the slot
+    layout of partial[] follows the chunks per lane, which AUTO picks from the CU count."""
     import ctypes
 
     from rti import _lib as L
@@ -164,8 +167,15 @@ def test_launch_generations_bit_identical(cuda, layout):
     lu, lv = o.synth_dirs(N, 9)
     g = torch.Generator(device=cuda).manual_seed(11)
     I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda).to(torch.float32)
-    A64 = torch.as_tensor(rti.design_matrix(lu, lv, "ptm"), device=cuda).contiguous()
-    G = torch.as_tensor(rti.gram_inverse(lu, lv, "ptm"), device=cuda).contiguous()
+    if form == "gram":
+        A64 = torch.as_tensor(rti.design_matrix(lu, lv, "ptm"), device=cuda).contiguous()
+        G = torch.as_tensor(rti.gram_inverse(lu, lv, "ptm"), device=cuda).contiguous()
+        fn = L.lib().rti_fit_shared_residual
+    else:
+        U, Wf = rti.lsq_factors(lu, lv, "ptm")
+        A64 = torch.as_tensor(U, device=cuda).contiguous()
+        G = torch.as_tensor(Wf, device=cuda).contiguous()
+        fn = L.lib().rti_fit_shared_residual_svd
     lib = L.lib()
     nb = int(lib.rti_fit_shared_residual_blocks(P))
     s = ctypes.c_void_p(torch.cuda.current_stream(cuda).cuda_stream)
@@ -175,8 +185,8 @@ def test_launch_generations_bit_identical(cuda, layout):
         coef = torch.full((C, P, k) if layout == "pixel" else (C, k, P), float("nan"), device=cuda)
         res = torch.full((C, P), float("nan"), device=cuda)
         part = torch.zeros((C, nb), dtype=torch.float64, device=cuda)
-        st = lib.rti_fit_shared_residual(vp(A64), vp(G), k, N, vp(I), L.RTI_F32, P, C, P, N * P, vp(coef),
-                                         rti.api._layout_id(layout), P * k, vp(res), vp(part), flags, s)
+        st = fn(vp(A64), vp(G), k, N, vp(I), L.RTI_F32, P, C, P, N * P, vp(coef), rti.api._layout_id(layout), P * k,
+                vp(res), vp(part), flags | (3 << L.RTI_KERNEL_CHUNKS_SHIFT), s)
         L.check(st, "rti_fit_shared_residual")
         outs.append((coef, res, part, int(lib.rti_last_launch_count())))
     torch.cuda.synchronize()
@@ -189,3 +199,34 @@ def test_launch_generations_bit_identical(cuda, layout):
     for c in range(C):
         cc = ca[c][idx] if layout == "pixel" else ca[c][:, idx].T
         check(cc.cpu().numpy(), ra[c][idx].cpu().numpy(), None, I[c][:, idx].double().cpu().numpy(), "ptm", lu, lv, k)
+
+
+@pytest.mark.parametrize("planar", [False, True])
+def test_torch_op_fit_shared_residual(cuda, planar):
+    """torch.ops.rti.fit_shared_residual(U, W, I) -> (coef, res, partial): the same call as
+    rti.fit_with_residual, against the reference's golden coefficients and the fp64 oracle, plus the
+    fake-tensor registration (torch.library.opcheck: schema, fake vs real shapes/dtypes)."""
+    from rti import ops  # noqa: F401  registers torch.ops.rti.*
+
+    d = golden("ptm_shared_256x256_N20.npz")
+    N = 20
+    I = torch.as_tensor(d["I"], device=cuda).to(torch.float32).reshape(N, -1)
+    U, W = (torch.as_tensor(a, device=cuda) for a in rti.lsq_factors(d["lu"], d["lv"]))
+    coef, res, partial = torch.ops.rti.fit_shared_residual(U, W, I, planar)
+    c = coef.T.cpu().numpy() if planar else coef.cpu().numpy()
+    err, ok = coef_close(c.reshape(d["coef"].shape), d["coef"], rtol=1e-6)  # analysis.py:293-298
+    assert ok, err
+    c2, r2, rms2 = rti.fit_with_residual(I, d["lu"], d["lv"], layout="planar" if planar else "pixel")
+    assert torch.equal(coef, c2) and torch.equal(res, r2)
+    P = I.shape[1]
+    assert partial.shape == (int(rti._lib.lib().rti_fit_shared_residual_blocks(P)),)
+    assert abs(float(torch.sqrt(partial.sum() / (P * N))) - float(rms2)) <= 1e-12 * float(rms2)
+    check(c, res.cpu().numpy(), float(rms2), np.asarray(d["I"], np.float64).reshape(N, -1), "ptm", d["lu"], d["lv"], 6)
+    # 3-D (channels) form and the fake kernel
+    I3 = torch.stack([I, I.flip(1)])
+    coef3, res3, part3 = torch.ops.rti.fit_shared_residual(U, W, I3, planar)
+    assert torch.equal(coef3[0], coef) and torch.equal(res3[0], res)
+    torch.library.opcheck(torch.ops.rti.fit_shared_residual.default, (U, W, I3, planar, 0),
+                          test_utils=("test_schema", "test_faketensor"))
+    with pytest.raises(ValueError):
+        torch.ops.rti.fit_shared_residual(U.float(), W, I, planar)

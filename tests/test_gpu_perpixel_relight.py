@@ -205,6 +205,10 @@ def test_compat_compute_end_to_end(cuda, tmp_path, ptm):
     print(f"compute({'PTM' if ptm else 'RBF'}) tables: {int(diff.sum())} of {diff.size} entries differ "
           f"from the reference")
     assert not (diff & ~np.transpose(near, (2, 3, 0, 1))).any()
+    if ptm:
+        # the fused per-pixel fit's light vectors are bit-exact (rti_perpixel.hip light_dir_fast + refine), so
+        # the int32 tables equal the reference's entry for entry
+        assert not diff.any(), int(diff.sum())
 
 
 @pytest.mark.parametrize("basis", ["ptm", "hsh9", "hsh"])
@@ -229,3 +233,28 @@ def test_relight_staged_rows_bit_identical_to_planar(cuda, basis, cdt):
     fa = rti.relight_frame(coef, hsv, 0.3, -0.25, basis=basis)
     fb = rti.relight_frame(planar, hsv, 0.3, -0.25, basis=basis, layout="planar")
     assert torch.equal(fa, fb)
+
+
+@pytest.mark.parametrize("H,W,N", [(32, 32, 50), (300, 257, 100)])
+def test_perpixel_cam_light_vectors_bit_exact(cuda, H, W, N):
+    """fit_perpixel_cam generates compute_intensities' light vectors in-kernel (rsq + Newton, with pixels
+    near an fp32 rounding midpoint sent to the exact refine pass): its coefficients equal those of
+    fit_perpixel_dirs fed the bit-exact rti_light_dirs output — bit for bit on every pixel the refine pass
+    did not redo (those few are re-solved by QR, within 1e-12)."""
+    if N == 50:
+        d = golden("ptm_perpixel_32x32_N50.npz")
+        cams, frames = d["cams"], np.ascontiguousarray(d["frames"])
+    else:
+        rng = np.random.default_rng(3)
+        cams = np.stack([rng.uniform(-300, 600, N), rng.uniform(-300, 600, N), rng.uniform(100, 500, N)], -1)
+        frames = rng.integers(0, 256, (N, H, W)).astype(np.uint8)
+    I = torch.as_tensor(frames, device=cuda)
+    a = rti.fit(I, cams=cams, mode="perpixel", coef_dtype=torch.float64)
+    lu, lv = rti.light_dirs(cams, H, W, device=cuda)
+    b = rti.fit(I.permute(1, 2, 0).contiguous(), lu, lv, mode="perpixel", coef_dtype=torch.float64)
+    same = (a == b).all(-1)
+    frac = float(same.double().mean())
+    err, ok = coef_close(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-12)
+    print(f"cam vs dirs {H}x{W}x{N}: {frac:.6f} of pixels bit-identical, the rest within {err:.2g}")
+    assert ok, err
+    assert frac >= 0.999, frac
