@@ -830,10 +830,48 @@ def cpu_baseline(wl, budget_s):
 
 # ---- multi-GPU legs ---------------------------------------------------------------------------
 
+def cyclic_stack(wl, ctx, chunks):
+    """This rank's rows under the block-cyclic partition (rti.parallel.cyclic_rows), generated on the
+    device block by block exactly as the block rows are (synth_stack is a function of the global rows),
+    as a light-major [N, h, W] stack of channel 0 in the workload's intensity dtype."""
+    import torch
+
+    from rti.parallel import cyclic_rows
+
+    blocks = cyclic_rows(ctx.H, ctx.world, ctx.rank, chunks)
+    parts = [synth_stack(ctx.H, wl.W, wl.N, 1, wl.basis, wl.lu, wl.lv, seed=1000, device=ctx.dev, rows=b)[0]
+             for b in blocks]
+    I = torch.cat(parts, dim=1).reshape(wl.N, -1, wl.W)
+    return I.to(wl.I.dtype) if I.dtype != wl.I.dtype else I
+
+
+def e2e_parity(wl, ctx, full, chunks, per_block=256):
+    """Rank 0: sampled pixels of EVERY row block of the gathered [H, W, k] map (all ranks' blocks, block-
+    cyclic order) against the oracle on that block's regenerated intensities — checks the fit and that
+    every block landed in its place."""
+    from rti.parallel import cyclic_rows
+
+    o = oracle()
+    worst, checked = 0.0, 0
+    for r in range(ctx.world):
+        for bi, (r0, r1) in enumerate(cyclic_rows(ctx.H, ctx.world, r, chunks)):
+            I = synth_stack(ctx.H, wl.W, wl.N, 1, wl.basis, wl.lu, wl.lv, seed=1000, device=ctx.dev, rows=(r0, r1))[0]
+            if wl.in_bytes == 1:
+                I = I.to(wl.I.dtype)
+            idx = sample_idx((r1 - r0) * wl.W, per_block, 17 + 31 * r + bi)
+            ref = o.fit_shared(I[:, idx].float().cpu().numpy(), wl.pinv64)
+            got = full[r0:r1].reshape(-1, wl.k)[idx].cpu().numpy()
+            worst = max(worst, coef_parity(got, ref))
+            checked += len(idx)
+    return {"max_rel": worst, "tol": 1e-4, "ok": bool(worst <= 1e-4), "checked_px": checked,
+            "blocks": ctx.world * chunks, "vs": "oracle fit_shared on each block's regenerated rows"}
+
+
 def allgather_legs(wl, ctx, reps=5):
     """RCCL all-gather of this rank's coefficient rows into the whole [H, W, k] map, and the row-chunked
     fit with each chunk's all-gather overlapped with the next chunk's fit (block-cyclic rows, so every
-    chunk lands in place).  Returns (allgather_ms, overlapped_ms) maxed over ranks."""
+    chunk lands in place; this rank's cyclic rows are generated for it).  Returns (allgather_ms,
+    overlapped_ms, chunks, e2e parity of the overlapped map; rank 0 checks, others None)."""
     import torch
     import torch.distributed as dist
 
@@ -851,19 +889,24 @@ def allgather_legs(wl, ctx, reps=5):
         gather_rows(local, ctx.H)
     torch.cuda.synchronize(dev)
     gather_ms = (time.perf_counter() - t0) / reps * 1e3
-    chunks = next(c for c in (4, 3, 2, 1) if ctx.h % c == 0)  # cyclic blocks of h/chunks rows (2160/8 = 270: 3)
-    fitter = RowTiledFitter(wl.I[0].reshape(wl.N, ctx.h, wl.W), wl.lu, wl.lv, ctx.H, basis=wl.basis, chunks=chunks,
-                            partition="cyclic")
+    # cyclic blocks of H/(G*chunks) rows (4K on 8 GPUs: 2160/8 = 270 rows per rank -> 3 chunks of 90)
+    chunks = next(c for c in (4, 3, 2, 1) if ctx.H % (ctx.world * c) == 0)
+    I_cyc = cyclic_stack(wl, ctx, chunks)
+    fitter = RowTiledFitter(I_cyc, wl.lu, wl.lv, ctx.H, basis=wl.basis, chunks=chunks, partition="cyclic")
     for _ in range(2):
         fitter()
     torch.cuda.synchronize(dev)
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        fitter()
+        full = fitter()
     torch.cuda.synchronize(dev)
     e2e_ms = (time.perf_counter() - t0) / reps * 1e3
-    return gather_ms, e2e_ms, chunks
+    par = None
+    if not wl.args.no_parity and ctx.rank == 0:
+        par = e2e_parity(wl, ctx, full, chunks)
+    del I_cyc, fitter
+    return gather_ms, e2e_ms, chunks, par
 
 
 def device_info(dev):
@@ -918,6 +961,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-budget", type=float, default=16.0, help="seconds of CPU baseline (half per thread count)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo lets ranks share one GPU in rehearsals")
+    ap.add_argument("--shape", default=None,
+                    help="HxW override of the config's image (rehearsals and tests only; the line's config says it)")
     ap.add_argument("--plan", action="store_true",
                     help="print the rank/row plan only (no device work; CPU tests of the launcher)")
     return ap.parse_args(argv)
@@ -927,6 +972,9 @@ def main():
     args = parse_args()
     maybe_spawn(args)
     cfg = CONFIGS[args.config]
+    if args.shape:
+        h, w = (int(x) for x in args.shape.lower().split("x"))
+        cfg = (cfg[0], h, w) + cfg[3:6] + (cfg[6] + f" [shape override {h}x{w}]",)
     kind = cfg[0]
     if args.steps is None:
         args.steps = DEFAULT_STEPS[kind]
@@ -1027,9 +1075,10 @@ def main():
             parity["ok"] = worst[1] == 0.0
             parity["ranks"] = world
 
-    gather_ms = e2e_ms = None
+    gather_ms = e2e_ms = e2e_par = None
     if world > 1 and kind == "fit" and not args.no_allgather:
-        gather_ms, e2e_ms, n_chunks = reduce_max(list(allgather_legs(wl, ctx)), ctx, backend)
+        gather_ms, e2e_ms, n_chunks, e2e_par = allgather_legs(wl, ctx)
+        gather_ms, e2e_ms = reduce_max([gather_ms, e2e_ms], ctx, backend)
 
     value = wl.total_units * args.steps / elapsed / 1e6
     cpu = None
@@ -1070,6 +1119,7 @@ def main():
             line["fit_allgather_overlapped_ms"] = round(e2e_ms, 3)  # row chunks, gather(c) || fit(c+1)
             line["overlap_chunks"] = int(n_chunks)
             line["end_to_end_Mpix_lights_per_s"] = round(wl.total_units / (e2e_ms * 1e-3) / 1e6, 1)
+            line["e2e_parity"] = e2e_par
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

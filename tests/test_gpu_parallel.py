@@ -65,3 +65,27 @@ def test_rowtiled_fit_two_ranks_one_gpu(cuda):
         assert p.exitcode == 0
     for rank, shape, same, err in results:
         assert shape == (37, 64, 6) and same and err < 1e-4, (rank, shape, same, err)
+
+
+@pytest.mark.parametrize("gpus,shape,extra", [(2, "96x128", []), (3, "90x64", ["--in-dtype", "u8"]),
+                                              (2, "64x96", ["--weak"])])
+def test_bench_multi_rank_end_to_end_parity(cuda, gpus, shape, extra):
+    """bench.py --gpus N (ranks sharing cuda:0 over gloo): the strong-scaling line, the all-gather legs and
+    the overlapped row-chunked fit whose gathered map (block-cyclic rows generated per rank) rank 0 checks
+    block by block against the oracle (e2e_parity)."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--dist-backend", "gloo",
+                        "--config", "c2", "--shape", shape, "--steps", "2", "--warmup", "1", "--no-cpu"] + extra,
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == gpus and line["parity"]["ok"], line["parity"]
+    e2e = line["e2e_parity"]
+    assert e2e["ok"] and e2e["blocks"] == gpus * line["overlap_chunks"] and e2e["checked_px"] > 0, e2e
