@@ -139,6 +139,26 @@ int rti_fit_shared(const float* pinv, int k, int N,
                    float* coef, int coef_layout, int64_t coef_channel_stride,
                    int kernel, rti_stream_t stream);
 
+/* ---- 8-bit stacks: the shared fit on the int8 matrix cores -------------------------
+ * The reference's intensities are the uint8 V channel (FeatureMatcher.py:183-184, analysis.py:219).
+ * rti_q8_operator (host) turns an fp64 operator pinv[k][N] (rti_pinv) into the fixed-point form the
+ * kernel reads: each row scaled to 27-bit fixed point and split into four int8 digits laid out as
+ * v_mfma_i32_16x16x64_i8 A fragments, plus per-row scales and sign-flip corrections (layout:
+ * smartphone-based-rti_amd/csrc/rti_q8.h).  op must hold rti_q8_operator_bytes(k, N) bytes; it is copied
+ * to the device by the caller (16-byte aligned).  Non-finite pinv entries (an exactly rank-deficient light
+ * set without rcond) return RTI_ERR_BAD_ARG: those fits keep the fp32 path and its NaN semantics.
+ * rti_fit_shared_q8 = rti_fit_shared for U8 stacks: coef[c][p][i] = Σ_n pinv[i][n]·I[c][n][p] with the
+ * digit products summed exactly in int32 and combined in fp64 (|Δc_i| <= 2^-28·max_n|pinv[i][n]|·Σ_n I_n,
+ * then one fp32 rounding), k ∈ {6, 9, 16}, N <= rti_fit_shared_q8_max_lights().  P, strides, I, op and
+ * coef 16-byte aligned (else RTI_ERR_UNSUPPORTED).  kernel: RTI_KERNEL_ONE_LAUNCH or 0 (AUTO). */
+int64_t rti_q8_operator_bytes(int k, int N);
+int rti_q8_operator(const double* pinv, int k, int N, void* op);
+int rti_fit_shared_q8_max_lights(void);
+int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I, int64_t P, int C,
+                      int64_t light_stride, int64_t channel_stride,
+                      float* coef, int coef_layout, int64_t coef_channel_stride,
+                      int kernel, rti_stream_t stream);
+
 /* ---- device: per-pixel residuals of the shared-direction fit -----------------------
  * Fit quality next to rti_fit_shared's coefficients (the reference computes the same
  * least-squares solution, analysis.py:280-298, and never reports its residual):

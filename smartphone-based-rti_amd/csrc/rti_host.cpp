@@ -15,6 +15,7 @@
 
 #include "rti_basis.h"
 #include "rti_internal.h"
+#include "rti_q8.h"
 
 namespace rti {
 
@@ -271,6 +272,58 @@ int rti_lsq_factors(int basis, const float* lu, const float* lv, int n, double r
   std::vector<double> A((size_t)n * k);
   for (int i = 0; i < n; ++i) design_row(basis, lu[i], lv[i], &A[(size_t)i * k]);
   jacobi_pinv(A.data(), n, k, rcond, nullptr, nullptr, U, W);
+  return RTI_OK;
+}
+
+int64_t rti_q8_operator_bytes(int k, int N) {
+  if (k < 1 || k > 16 || N <= 0) return -1;
+  return q8_operator_bytes(N);
+}
+
+int rti_q8_operator(const double* pinv, int k, int N, void* op) {
+  if (!pinv || !op) return fail(RTI_ERR_BAD_ARG, "rti_q8_operator: null pointer");
+  if (k < 1 || k > 16 || N <= 0) return fail(RTI_ERR_BAD_ARG, "rti_q8_operator: k=%d N=%d", k, N);
+  const int T = q8_steps(N);
+  int8_t* frag = static_cast<int8_t*>(op);
+  double* scale = reinterpret_cast<double*>(static_cast<char*>(op) + q8_frag_bytes(N));
+  int32_t* corr = reinterpret_cast<int32_t*>(scale + 16);
+  std::vector<int8_t> dig((size_t)Q8_DIGITS * k * N);  // dig[j][i][n]
+  for (int i = 0; i < 16; ++i) {
+    scale[i] = 0.0;
+    for (int j = 0; j < Q8_DIGITS; ++j) corr[i * Q8_DIGITS + j] = 0;
+  }
+  for (int i = 0; i < k; ++i) {
+    double m = 0.0;
+    for (int n = 0; n < N; ++n) {
+      const double w = pinv[(size_t)i * N + n];
+      if (!std::isfinite(w))
+        return fail(RTI_ERR_BAD_ARG, "rti_q8_operator: non-finite pseudo-inverse entry (row %d, light %d)", i, n);
+      m = std::fmax(m, std::fabs(w));
+    }
+    scale[i] = m * 0x1p-27;
+    for (int n = 0; n < N; ++n) {
+      int64_t W = m > 0.0 ? (int64_t)std::llround(pinv[(size_t)i * N + n] / m * 0x1p27) : 0;  // |W| <= 2^27
+      int8_t d[Q8_DIGITS];
+      for (int j = Q8_DIGITS - 1; j > 0; --j) {  // balanced base-128 digits, least significant first
+        const int64_t r = ((W + 64) % 128 + 128) % 128 - 64;
+        d[j] = (int8_t)r;
+        W = (W - r) / 128;
+      }
+      d[0] = (int8_t)W;  // in [-64, 64]
+      for (int j = 0; j < Q8_DIGITS; ++j) {
+        dig[((size_t)j * k + i) * N + n] = d[j];
+        corr[i * Q8_DIGITS + j] += 128 * d[j];
+      }
+    }
+  }
+  for (int t = 0; t < T; ++t)
+    for (int j = 0; j < Q8_DIGITS; ++j)
+      for (int l = 0; l < 64; ++l)
+        for (int e = 0; e < 16; ++e) {
+          const int i = l & 15, n = t * Q8_STEP + q8_light(l >> 4, e);
+          frag[(((size_t)t * Q8_DIGITS + j) * 64 + l) * 16 + e] =
+              (i < k && n < N) ? dig[((size_t)j * k + i) * N + n] : (int8_t)0;
+        }
   return RTI_OK;
 }
 

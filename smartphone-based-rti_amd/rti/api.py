@@ -116,6 +116,41 @@ def lsq_factors(lu, lv, basis="ptm", rcond=None):
     return U, W
 
 
+def q8_operator(pinv64):
+    """Host: the fixed-point int8-digit form of an fp64 operator [k, N] for ``rti_fit_shared_q8`` (8-bit
+    stacks on the int8 matrix cores; layout in csrc/rti_q8.h).  Raises ValueError for non-finite entries."""
+    pv = np.ascontiguousarray(np.asarray(pinv64, np.float64))
+    k, N = pv.shape
+    nb = int(L.lib().rti_q8_operator_bytes(k, N))
+    if nb <= 0:
+        raise ValueError(f"no q8 operator for k={k}, N={N}")
+    op = np.zeros(nb, dtype=np.uint8)
+    L.check(L.lib().rti_q8_operator(_dptr(pv), k, N, ctypes.c_void_p(op.ctypes.data)), "rti_q8_operator")
+    return op
+
+
+def q8_supported(I, k, N):
+    """Whether ``rti_fit_shared_q8`` takes this stack (uint8, k in {6, 9, 16}, N within its LDS budget,
+    16-byte aligned planes)."""
+    if I.dtype != torch.uint8 or k not in (6, 9, 16) or N > int(L.lib().rti_fit_shared_q8_max_lights()):
+        return False
+    P = I.shape[-1] if I.dim() == 2 else I.shape[-1] * I.shape[-2]
+    return P % 16 == 0 and I.data_ptr() % 16 == 0
+
+
+def fit_q8_into(op_dev, I, coef, *, k, layout="pixel", flags=0):
+    """Launch ``rti_fit_shared_q8`` on preallocated tensors: op_dev = q8_operator(...) on the device (uint8),
+    I a contiguous uint8 CUDA [N, P] or [C, N, P] stack, coef fp32 as fit_shared_into."""
+    if I.dim() == 2:
+        C, (N, P) = 1, I.shape
+    else:
+        C, N, P = I.shape
+    st = L.lib().rti_fit_shared_q8(_vp(op_dev), k, N, _vp(I), P, C, P, N * P, _vp(coef), _layout_id(layout), P * k,
+                                   int(flags), _stream_of(I))
+    L.check(st, "rti_fit_shared_q8")
+    return coef
+
+
 def basis_eval(lu, lv, basis="ptm"):
     """Host fp64 basis values [E, k] at (lu, lv)."""
     lu = np.ascontiguousarray(np.asarray(lu, np.float64).ravel())
@@ -205,11 +240,21 @@ def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=Non
         pv = pinv(lu, lv, b, rcond)
         if pv.shape[1] != N:
             raise ValueError(f"{pv.shape[1]} light directions for {N} intensity planes")
-        pinv_dev = torch.as_tensor(pv.astype(np.float32), device=I.device)
         Ic = I.contiguous().reshape(C, N, P)
         shape = (C, P, k) if cl == L.RTI_COEF_PIXEL_MAJOR else (C, k, P)
         coef = torch.empty(shape, dtype=torch.float32, device=I.device)
-        fit_shared_into(pinv_dev, Ic, coef, k=k, layout=cl, kernel=kernel, nontemporal=nontemporal)
+        # 8-bit stacks (the reference's V channel): the int8-MFMA fixed-point fit when the operator is finite
+        # (a rank-deficient light set without rcond keeps the fp32 path and the reference's NaN)
+        if kernel in ("auto", "q8") and q8_supported(Ic, k, N) and np.isfinite(pv).all():
+            op_dev = torch.as_tensor(q8_operator(pv), device=I.device)
+            fit_q8_into(op_dev, Ic, coef, k=k, layout=cl)
+        elif kernel == "q8":
+            raise NotImplementedError("kernel='q8' needs a uint8 stack, k in (6, 9, 16), N <= "
+                                      f"{int(L.lib().rti_fit_shared_q8_max_lights())}, 16-pixel-aligned planes and a "
+                                      "finite pseudo-inverse")
+        else:
+            pinv_dev = torch.as_tensor(pv.astype(np.float32), device=I.device)
+            fit_shared_into(pinv_dev, Ic, coef, k=k, layout=cl, kernel=kernel, nontemporal=nontemporal)
         if cl == L.RTI_COEF_PIXEL_MAJOR:
             out = coef.reshape((C,) + spatial + (k,))
         else:

@@ -148,3 +148,51 @@ def test_lsq_factors_rank_deficient_and_rcond():
     assert np.abs(W @ U.T - ref).max() < 1e-10 * np.abs(ref).max()
     with pytest.raises(ValueError):
         rti.lsq_factors(e["singular_lu"][:5], e["singular_lv"][:5])
+
+
+def _q8_decode(op, k, N):
+    """Read rti_q8_operator's buffer back (layout of csrc/rti_q8.h): digits [4, k, N], scale [k], corr [k, 4]."""
+    T = (N + 63) // 64
+    frag = op[: T * 4 * 64 * 16].view(np.int8).reshape(T, 4, 64, 16)
+    scale = op[T * 4096: T * 4096 + 128].view(np.float64)
+    corr = op[T * 4096 + 128: T * 4096 + 128 + 256].view(np.int32).reshape(16, 4)
+    light = lambda g, e: 8 * g + e if e < 8 else 32 + 8 * g + (e - 8)  # noqa: E731
+    dig = np.zeros((4, 16, T * 64), np.int64)
+    for lane in range(64):
+        i, g = lane & 15, lane >> 4
+        for e in range(16):
+            dig[:, i, np.arange(T) * 64 + light(g, e)] = frag[:, :, lane, e].T
+    assert not dig[:, k:].any() and not dig[:, :, N:].any()  # padding rows / lights are zero
+    return dig[:, :k, :N], scale[:k], corr[:k]
+
+
+@pytest.mark.parametrize("basis,N", [("ptm", 20), ("ptm", 100), ("hsh", 200), ("hsh9", 65), ("ptm", 6)])
+def test_q8_operator_fixed_point_digits(basis, N):
+    """rti_q8_operator (host): four balanced int8 digits per weight reconstruct the 27-bit fixed-point
+    operator, the sign-flip corrections are 128·Σ digits, and the exact integer evaluation the kernel does
+    (int32 digit sums of x − 128, fp64 combination) reproduces pinv·I to the 2^-28 quantization bound."""
+    lu, lv = o.synth_dirs(N, 7)
+    pv = rti.pinv(lu, lv, basis)
+    k = pv.shape[0]
+    op = rti.q8_operator(pv)
+    assert op.size == rti._lib.lib().rti_q8_operator_bytes(k, N)
+    dig, scale, corr = _q8_decode(op, k, N)
+    assert dig[1:].min() >= -64 and dig[1:].max() <= 63 and np.abs(dig[0]).max() <= 64
+    W = ((dig[0] * 128 + dig[1]) * 128 + dig[2]) * 128 + dig[3]
+    m = np.abs(pv).max(1)
+    assert np.allclose(scale, m * 2.0 ** -27, rtol=0, atol=0)
+    assert np.abs(W * scale[:, None] - pv).max() <= m.max() * 2.0 ** -28 * 1.0000001
+    assert np.array_equal(corr, 128 * dig.sum(-1).T)
+    I = np.random.default_rng(N).integers(0, 256, (N, 777))
+    acc = np.einsum("jin,np->jip", dig, I - 128)
+    s = acc + corr.T[:, :, None]
+    c = (((s[0] * 128 + s[1]) * 128 + s[2]) * 128 + s[3]) * scale[:, None]
+    ref = pv @ I
+    bound = 2.0 ** -28 * m[:, None] * I.sum(0)[None, :]
+    assert (np.abs(c - ref) <= bound * 1.0000001 + 1e-12 * np.abs(ref)).all()
+
+
+def test_q8_operator_rejects_non_finite():
+    e = golden("ptm_edge.npz")
+    with pytest.raises(ValueError, match="non-finite"):
+        rti.q8_operator(rti.pinv(e["singular_lu"], e["singular_lv"]))

@@ -1,0 +1,147 @@
+"""GPU parity of the 8-bit fit on the int8 matrix cores (rti_fit_shared_q8, AUTO for uint8 stacks in
+rti.fit): the reference's golden coefficients, the fp64 oracle over every supported basis, light counts
+around the 64-light steps and the LDS limit, ragged pixel counts (partial tiles), two channels, both
+layouts, launch generations, and the fallbacks (fp32 path) where q8 does not apply.
+
+Tolerance: the q8 operator's quantization bound is 2^-28·max_n|pinv|·Σ_n I_n (rti_q8.h), far below fp32
+rounding; coefficients are held to 1e-6 of max_k |c_ref,k| per pixel (the fp32 stream's bar is 1e-4)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import rti
+import rti_oracle as o
+from conftest import coef_close, golden
+from rti import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def fit_u8(I_np, lu, lv, basis, cuda, **kw):
+    return rti.fit(torch.as_tensor(I_np, device=cuda), lu, lv, basis=basis, **kw)
+
+
+def test_golden_256x256_N20(cuda):
+    d = golden("ptm_shared_256x256_N20.npz")
+    I = np.asarray(d["I"]).astype(np.uint8)
+    assert np.array_equal(I, d["I"])  # the golden stack is integer 0..255
+    coef = fit_u8(I, d["lu"], d["lv"], "ptm", cuda).cpu().numpy()
+    err, ok = coef_close(coef, d["coef"], rtol=1e-6)  # the reference's own coefficients (analysis.py:293-298)
+    print(f"q8 vs reference golden: {err:.3g}")
+    assert ok, err
+
+
+@pytest.mark.parametrize("basis", ["ptm", "hsh9", "hsh"])
+@pytest.mark.parametrize("N", [16, 63, 64, 65, 100, 200])
+@pytest.mark.parametrize("layout", ["pixel", "planar"])
+def test_vs_oracle(cuda, basis, N, layout):
+    k = rti.basis_terms(basis)
+    if N < k:
+        pytest.skip("N < k")
+    lu, lv = o.synth_dirs(N, N + k)
+    rng = np.random.default_rng(N * 31 + k)
+    for P in (16, 1024, 1040, 3 * 1024 + 16 * 7):
+        I = rng.integers(0, 256, size=(2, N, P), dtype=np.uint8)
+        coef = rti.fit(torch.as_tensor(I, device=cuda)[..., None], lu, lv, basis=basis, layout=layout).cpu().numpy()
+        pv = np.linalg.pinv(o.design("ptm" if basis == "ptm" else "hsh", lu, lv)[:, :k])
+        for c in range(2):
+            got = coef[c].reshape(P, k) if layout == "pixel" else coef[c].reshape(k, P).T
+            err, ok = coef_close(got, (pv @ I[c].astype(np.float64)).T, rtol=1e-6)
+            assert ok, (P, c, err)
+
+
+def test_max_lights_and_extremes(cuda):
+    Nmax = int(L.lib().rti_fit_shared_q8_max_lights())
+    assert Nmax >= 256
+    lu, lv = o.synth_dirs(Nmax, 5)
+    pv = o.pinv_shared("hsh", lu, lv)
+    for fill in (0, 255, None):
+        I = (np.full((Nmax, 2048), fill, np.uint8) if fill is not None
+             else np.random.default_rng(2).integers(0, 256, (Nmax, 2048), dtype=np.uint8))
+        coef = rti.fit(torch.as_tensor(I, device=cuda), lu, lv, basis="hsh").cpu().numpy()
+        ref = (pv @ I.astype(np.float64)).T
+        if fill == 0:
+            assert not coef.any()
+        else:
+            err, ok = coef_close(coef, ref, rtol=1e-6)
+            assert ok, (fill, err)
+
+
+def test_q8_matches_fp32_stream_and_is_used(cuda):
+    """AUTO on uint8 runs rti_fit_shared_q8 (its launch count is the q8 generations'), and agrees with the fp32
+    stream on the same stack within the fp32 stream's own rounding."""
+    lu, lv = o.synth_dirs(100, 2)
+    I = torch.as_tensor(o.synth_intensities(216, 384, lu, lv, seed=3), device=cuda).round().clamp(0, 255)
+    a = rti.fit(I.to(torch.uint8), lu, lv, kernel="q8")
+    b = rti.fit(I.to(torch.uint8), lu, lv, kernel="valu")
+    c = rti.fit(I, lu, lv)
+    err, ok = coef_close(a.cpu().numpy(), c.cpu().numpy(), rtol=1e-5)
+    assert ok, err
+    assert torch.equal(b, rti.fit(I.to(torch.uint8), lu, lv, kernel="valu"))
+    ref = o.fit_shared(I.reshape(100, -1).double().cpu().numpy(), o.pinv_shared("ptm", lu, lv)).reshape(a.shape)
+    ea, _ = coef_close(a.cpu().numpy(), ref)
+    eb, _ = coef_close(b.cpu().numpy(), ref)
+    print(f"u8 4K-slice: q8 {ea:.3g} vs fp32 VALU stream {eb:.3g} (max rel to fp64)")
+    assert ea <= 1e-6 and ea <= eb
+
+
+def test_launch_generations_bit_identical(cuda):
+    """AUTO splits a large q8 fit into launches over pixel ranges of whole 1024-pixel tiles; the result
+    equals RTI_KERNEL_ONE_LAUNCH's bit for bit (ragged P, 3 channels, HSH-16)."""
+    N, C, P = 200, 3, 1024 * 2100 + 16 * 5
+    lu, lv = o.synth_dirs(N, 4)
+    pv = o.pinv_shared("hsh", lu, lv)
+    op = torch.as_tensor(rti.q8_operator(pv), device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda, dtype=torch.uint8)
+    outs = []
+    for flags in (0, L.RTI_KERNEL_ONE_LAUNCH):
+        coef = torch.full((C, P, 16), float("nan"), device=cuda)
+        rti.api.fit_q8_into(op, I, coef, k=16, flags=flags)
+        outs.append((coef, int(L.lib().rti_last_launch_count())))
+    (a, la), (b, lb) = outs
+    assert la > 1 and lb == 1, (la, lb)
+    assert not torch.isnan(a).any() and torch.equal(a, b)
+    idx = torch.as_tensor(np.unique(np.r_[np.random.default_rng(1).integers(0, P, 512), 0, P - 1]), device=cuda)
+    for c in range(C):
+        ref = (pv @ I[c][:, idx].double().cpu().numpy()).T
+        err, ok = coef_close(a[c][idx].cpu().numpy(), ref, rtol=1e-6)
+        assert ok, (c, err)
+
+
+def test_fallbacks_keep_reference_semantics(cuda):
+    """Where q8 does not apply rti.fit keeps the fp32 stream: P % 16 != 0, N above the LDS limit, and an
+    exactly rank-deficient light set (NaN like the reference; the q8 operator refuses non-finite weights)."""
+    e = golden("ptm_edge.npz")
+    I = torch.as_tensor(np.tile(e["singular_I"].astype(np.uint8)[:, None], (1, 64)), device=cuda)
+    assert torch.isnan(rti.fit(I, e["singular_lu"], e["singular_lv"])).all()
+    with pytest.raises(NotImplementedError):
+        rti.fit(I, e["singular_lu"], e["singular_lv"], kernel="q8")
+    lu, lv = o.synth_dirs(30, 1)
+    I = np.random.default_rng(0).integers(0, 256, (30, 37), dtype=np.uint8)  # P % 16 != 0
+    coef = rti.fit(torch.as_tensor(I, device=cuda), lu, lv).cpu().numpy()
+    err, ok = coef_close(coef, o.fit_shared(I.astype(np.float64), o.pinv_shared("ptm", lu, lv)))
+    assert ok, err
+    Nbig = int(L.lib().rti_fit_shared_q8_max_lights()) + 1
+    lu, lv = o.synth_dirs(Nbig, 2)
+    I = np.random.default_rng(1).integers(0, 256, (Nbig, 64), dtype=np.uint8)
+    coef = rti.fit(torch.as_tensor(I, device=cuda), lu, lv).cpu().numpy()
+    err, ok = coef_close(coef, o.fit_shared(I.astype(np.float64), o.pinv_shared("ptm", lu, lv)))
+    assert ok, err
+
+
+def test_abi_errors(cuda):
+    lib = L.lib()
+    lu, lv = o.synth_dirs(20, 1)
+    op = torch.as_tensor(rti.q8_operator(o.pinv_shared("ptm", lu, lv)), device=cuda)
+    I = torch.zeros((20, 48), dtype=torch.uint8, device=cuda)
+    coef = torch.empty((48, 6), device=cuda)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    s = ctypes.c_void_p(torch.cuda.current_stream(cuda).cuda_stream)
+    assert lib.rti_fit_shared_q8(vp(op), 7, 20, vp(I), 48, 1, 48, 0, vp(coef), 0, 0, 0, s) == L.RTI_ERR_UNSUPPORTED
+    assert lib.rti_fit_shared_q8(vp(op), 6, 20, vp(I), 40, 1, 40, 0, vp(coef), 0, 0, 0, s) == L.RTI_ERR_UNSUPPORTED
+    assert lib.rti_fit_shared_q8(vp(op), 6, 5, vp(I), 48, 1, 48, 0, vp(coef), 0, 0, 0, s) == L.RTI_ERR_BAD_ARG
+    assert lib.rti_fit_shared_q8(None, 6, 20, vp(I), 48, 1, 48, 0, vp(coef), 0, 0, 0, s) == L.RTI_ERR_BAD_ARG
+    assert lib.rti_fit_shared_q8(vp(op), 6, 20, vp(I), 48, 1, 48, 0, vp(coef), 0, 0, 0, s) == L.RTI_OK
