@@ -258,21 +258,30 @@ class FitWorkload(Workload):
         self.unit = "Mpix*lights/s"
         self.dtype = "f32" if args.in_dtype == "f32" else f"{args.in_dtype} in / f32 compute"
         L = rti._lib
-        kern = rti.api._KERNELS[args.kernel] | (L.RTI_KERNEL_NONTEMPORAL if args.nontemporal else 0)
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        fn = L.lib().rti_fit_shared
-        cargs = (ctypes.c_void_p(self.pinv_dev.data_ptr()), k, N, ctypes.c_void_p(self.I.data_ptr()),
-                 rti.api._IN_DTYPES[self.I.dtype], P, C, P, N * P, ctypes.c_void_p(self.coef.data_ptr()),
-                 rti.api._layout_id(args.layout), P * k, kern, stream)
+        self.q8 = args.kernel in ("auto", "q8") and rti.api.q8_supported(self.I, k, N, P)
+        if self.q8:  # 8-bit stacks: rti.fit's AUTO path, the int8-MFMA fixed-point fit (rti_fit_q8.hip)
+            self.op_dev = torch.as_tensor(rti.q8_operator(self.pinv64), device=dev)
+            fn, fname = L.lib().rti_fit_shared_q8, "rti_fit_shared_q8"
+            cargs = (ctypes.c_void_p(self.op_dev.data_ptr()), k, N, ctypes.c_void_p(self.I.data_ptr()), P, C, P, N * P,
+                     ctypes.c_void_p(self.coef.data_ptr()), rti.api._layout_id(args.layout), P * k, 0, stream)
+        else:
+            kern = rti.api._KERNELS[args.kernel] | (L.RTI_KERNEL_NONTEMPORAL if args.nontemporal else 0)
+            fn, fname = L.lib().rti_fit_shared, "rti_fit_shared"
+            cargs = (ctypes.c_void_p(self.pinv_dev.data_ptr()), k, N, ctypes.c_void_p(self.I.data_ptr()),
+                     rti.api._IN_DTYPES[self.I.dtype], P, C, P, N * P, ctypes.c_void_p(self.coef.data_ptr()),
+                     rti.api._layout_id(args.layout), P * k, kern, stream)
 
         def step(i):
             st = fn(*cargs)
             if st:
-                L.check(st, "rti_fit_shared")
+                L.check(st, fname)
 
         self.step = step
         step(0)
         self.launches = int(L.lib().rti_last_launch_count())
+        if self.q8:
+            self.dtype = "u8 in / int8 MFMA on a 4-digit 27-bit fixed-point operator, exact int32 sums / f32 out"
 
     def traffic(self):
         if self.ctx.world != 1 or self.ctx.weak:
@@ -283,7 +292,8 @@ class FitWorkload(Workload):
 
     def config(self):
         return {"lights": self.N, "channels": self.C, "basis": self.basis, "k": self.k,
-                "coef_layout": self.args.layout, "kernel": self.args.kernel, "intensity_dtype": self.args.in_dtype}
+                "coef_layout": self.args.layout, "kernel": "q8" if self.q8 else self.args.kernel,
+                "intensity_dtype": self.args.in_dtype}
 
     def coef_pk(self, c):
         cc = self.coef[c]
@@ -946,7 +956,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--weak", action="store_true", help="every rank fits a whole H-row image (weak scaling)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma", "tile"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma", "tile", "q8"])
     ap.add_argument("--layout", default="pixel", choices=["pixel", "planar"])
     ap.add_argument("--nontemporal", action="store_true")
     ap.add_argument("--in-dtype", default="f32", choices=["f32", "u8", "i32"],

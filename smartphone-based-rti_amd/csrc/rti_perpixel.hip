@@ -69,49 +69,51 @@ __device__ __forceinline__ void ne_add(Normal6& ne, float lu, float lv, double L
 __device__ __forceinline__ void ne_finish(Normal6& ne, int N) { ne.m[tri(5, 5)] = (double)N; }
 
 // compute_intensities' direction l = d / ‖d‖ (analysis.py:228-229), components rounded to fp32
-// (:230-231), BIT-EXACT with the reference's arrays at almost the cost of an rsq: the reference rounds
+// (:230-231), BIT-EXACT with the reference's arrays at the cost of an rsq: the reference rounds
 // s = (dx² + dy²) + dz² op by op, n = sqrt(s) and q = dx / n correctly (IEEE fp64), then q to fp32.
-// Here s is formed the same way (no contraction), 1/√s is the v_rsq_f64 seed refined by two Newton
-// steps, and q̃ = dx·(1/√s) lies within a few fp64 ulps of q.  fp32 rounding looks only at the low 29
-// bits of q's fp64 significand, so fp32(q̃) == fp32(q) unless q̃ lies within those few ulps of an fp32
-// rounding midpoint (low 29 bits = 2^28) — then (≈1 in 4·10⁶ lights) the pixel is marked and the
-// refine pass recomputes its light vectors with the IEEE sqrt and divide of rti_light_dirs.  Pinned by
-// tests/golden/ptm_perpixel_32x32_N50.npz through
-// rti_fit_perpixel_cam (test_gpu_perpixel_relight.py).
-__device__ __forceinline__ bool near_f32_midpoint(double q) {
-  constexpr uint32_t MARGIN = 64;  // fp64 ulps: the Newton-refined quotient is within ~4 of IEEE's
-  const uint32_t lo = (uint32_t)__double_as_longlong(q) & 0x1FFFFFFFu;
-  return lo - (0x10000000u - MARGIN) < 2 * MARGIN;
+// Here s = fma(dx, dx, fma(dy, dy, dz²)) (within 2 ulps of the reference's s), 1/√s is the v_rsq_f64 seed
+// refined by Newton steps, and q̃ = dx·(1/√s) lies within a few fp64 ulps of q.  fp32 rounding looks only
+// at the low 29 bits of q's fp64 significand, so fp32(q̃) == fp32(q) unless q̃ lies within those few
+// ulps of an fp32 rounding midpoint (low 29 bits = 2^28), or the fp32 result is subnormal.  The fast form
+// folds both tests into two running minima (mid_key == 0, or |l| < FLT_MIN, flags the light: ≈1 in
+// 4·10⁶ components), and a flagged pixel is re-solved by the refine pass, whose light_dir_exact uses the
+// IEEE sqrt and divide of rti_light_dirs.  Pinned by tests/golden/ptm_perpixel_32x32_N50.npz through
+// rti_fit_perpixel_cam (test_gpu_perpixel_relight.py); the ulp budget by tools/probe/rsq_probe.hip.
+constexpr uint32_t MID_MARGIN = 64;  // fp64 ulps: the Newton-refined quotient is within a few of IEEE's
+constexpr int NEWTON = 2;
+
+// 0 iff the low 29 significand bits of q lie within MID_MARGIN of 2^28 (an fp32 rounding midpoint)
+__device__ __forceinline__ uint32_t mid_key(double q) {
+  const uint32_t lo = (uint32_t)__double_as_longlong(q);
+  return (((lo ^ 0x10000000u) + MID_MARGIN) & 0x1FFFFFFFu) & ~(2 * MID_MARGIN - 1);
 }
 
-// The fast form: `ambiguous` is set when the lane's fp32 rounding could differ from the reference's
-// (a quotient near an fp32 midpoint, or s tiny/non-finite); the fit then marks the pixel and the refine
-// pass (light_dir_exact) redoes it, so the hot loop carries no sqrt/divide code.
-__device__ __forceinline__ void light_dir_fast(double dx, double dy, double dz, float& lu, float& lv,
-                                               bool& ambiguous) {
-#pragma clang fp contract(off)
-  const double s = dx * dx + dy * dy + dz * dz;  // (dx² + dy²) + dz², each op rounded
+struct DirCheck {
+  uint32_t key = 0xFFFFFFFFu;  // min of mid_key over the pixel's light components
+  float lmin = 1.0f;           // min of |l| (an fp32 subnormal or 0 result rounds on more bits)
+  __device__ __forceinline__ bool ambiguous() const { return key == 0 || !(lmin >= 0x1p-126f); }
+};
+
+__device__ __forceinline__ void light_dir_fast(double dx, double dy, double dz2, float& lu, float& lv,
+                                               DirCheck& chk) {
+  const double s = fma(dx, dx, fma(dy, dy, dz2));
   double y = __builtin_amdgcn_rsq(s);
   const double h = 0.5 * s;
-  y = fma(y, fma(-h * y, y, 0.5), y);
-  y = fma(y, fma(-h * y, y, 0.5), y);
+#pragma unroll
+  for (int i = 0; i < NEWTON; ++i) y = fma(y, fma(-h * y, y, 0.5), y);
   const double qx = dx * y, qy = dy * y;
-  // fp32 subnormal results round on more bits: |q| below 2^-120 (and not 0) is also ambiguous
-  ambiguous = ambiguous || near_f32_midpoint(qx) || near_f32_midpoint(qy) || !(s > 0x1p-900) ||
-              (fabs(qx) < 0x1p-120 && qx != 0.0) || (fabs(qy) < 0x1p-120 && qy != 0.0);
   lu = (float)qx;
   lv = (float)qy;
+  chk.key = min(chk.key, min(mid_key(qx), mid_key(qy)));
+  chk.lmin = fminf(chk.lmin, fminf(fabsf(lu), fabsf(lv)));
 }
 
+// the reference's arithmetic exactly (rti_light_dirs): separately rounded IEEE ops, no contraction
 __device__ __forceinline__ void light_dir_exact(double dx, double dy, double dz, float& lu, float& lv) {
 #pragma clang fp contract(off)
-  bool amb = false;
-  light_dir_fast(dx, dy, dz, lu, lv, amb);
-  if (amb) {
-    const double n = sqrt(dx * dx + dy * dy + dz * dz);
-    lu = (float)(dx / n);
-    lv = (float)(dy / n);
-  }
+  const double n = sqrt(dx * dx + dy * dy + dz * dz);
+  lu = (float)(dx / n);
+  lv = (float)(dy / n);
 }
 
 // Cholesky solve of (AᵀA) a = Aᵀb.  rcond < 0: singular only at a non-positive
@@ -296,16 +298,17 @@ fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I
   const double py = y0 + (double)(p / W);
   Normal6 ne;
   ne_zero(ne);
-  const T* __restrict__ src = I + p;
-  bool amb = false;
+  DirCheck chk;
+  const uint32_t po = (uint32_t)(p * (int64_t)sizeof(T));  // per-lane byte offset into each plane (< 2^32: launcher)
 #pragma unroll 4
   for (int n = 0; n < N; ++n) {
-    float lu, lv;  // cams: wave-uniform -> scalar loads
-    light_dir_fast(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv, amb);
-    ne_add(ne, lu, lv, ld_d(src + (int64_t)n * lstride));
+    float lu, lv;  // cams: wave-uniform -> scalar loads; the plane base is wave-uniform too
+    const double cz = cams[3 * n + 2];
+    light_dir_fast(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cz * cz, lu, lv, chk);
+    ne_add(ne, lu, lv, ld_d(reinterpret_cast<const T*>(reinterpret_cast<const char*>(I + (int64_t)n * lstride) + po)));
   }
   ne_finish(ne, N);
-  solve_store<TC, LAYOUT>(ne, rcond, coef, P, p, amb);
+  solve_store<TC, LAYOUT>(ne, rcond, coef, P, p, chk.ambiguous());
 }
 
 // Refine pass of fit_perpixel_cam: the marked pixels (ill-conditioned, or a light vector the fast form
@@ -459,6 +462,8 @@ extern "C" int rti_fit_perpixel_cam(const double* cams, int N, const void* I, in
                                     int coef_dtype, int coef_layout, rti_stream_t stream) {
   if (!cams) return fail(RTI_ERR_BAD_ARG, "rti_fit_perpixel_cam: null cams");
   if (H <= 0 || W <= 0) return fail(RTI_ERR_BAD_ARG, "rti_fit_perpixel_cam: H and W must be positive");
+  if ((int64_t)H * W * 4 >= ((int64_t)1 << 32))
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_perpixel_cam: H*W >= 2^30 pixels (32-bit plane byte offsets)");
   const int64_t P = (int64_t)H * W;
   int st = check_common("rti_fit_perpixel_cam", I, in_dtype, N, P, coef, coef_dtype, coef_layout);
   if (st != RTI_OK) return st;

@@ -129,12 +129,11 @@ def q8_operator(pinv64):
     return op
 
 
-def q8_supported(I, k, N):
-    """Whether ``rti_fit_shared_q8`` takes this stack (uint8, k in {6, 9, 16}, N within its LDS budget,
-    16-byte aligned planes)."""
+def q8_supported(I, k, N, P):
+    """Whether ``rti_fit_shared_q8`` takes this contiguous stack of P-pixel planes (uint8, k in {6, 9, 16}, N
+    within its LDS budget, 16-byte aligned planes)."""
     if I.dtype != torch.uint8 or k not in (6, 9, 16) or N > int(L.lib().rti_fit_shared_q8_max_lights()):
         return False
-    P = I.shape[-1] if I.dim() == 2 else I.shape[-1] * I.shape[-2]
     return P % 16 == 0 and I.data_ptr() % 16 == 0
 
 
@@ -245,7 +244,7 @@ def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=Non
         coef = torch.empty(shape, dtype=torch.float32, device=I.device)
         # 8-bit stacks (the reference's V channel): the int8-MFMA fixed-point fit when the operator is finite
         # (a rank-deficient light set without rcond keeps the fp32 path and the reference's NaN)
-        if kernel in ("auto", "q8") and q8_supported(Ic, k, N) and np.isfinite(pv).all():
+        if kernel in ("auto", "q8") and q8_supported(Ic, k, N, P) and np.isfinite(pv).all():
             op_dev = torch.as_tensor(q8_operator(pv), device=I.device)
             fit_q8_into(op_dev, Ic, coef, k=k, layout=cl)
         elif kernel == "q8":

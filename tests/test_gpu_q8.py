@@ -23,6 +23,16 @@ def fit_u8(I_np, lu, lv, basis, cuda, **kw):
     return rti.fit(torch.as_tensor(I_np, device=cuda), lu, lv, basis=basis, **kw)
 
 
+def q8_close(got, pv, I):
+    """The q8 contract (rti_q8.h): |c_i − (pinv·I)_i| <= 2^-28·max_n|pinv_in|·Σ_n I_n + one fp32 rounding.
+    got [P, k], pv [k, N] fp64, I [N, P] -> max error relative to max_k |c_ref,k| (reported)."""
+    ref = (pv @ I.astype(np.float64)).T
+    bound = 2.0 ** -28 * np.abs(pv).max(1)[None, :] * I.sum(0).astype(np.float64)[:, None] + 2.0 ** -24 * np.abs(ref)
+    diff = np.abs(np.asarray(got, np.float64) - ref)
+    assert (diff <= bound * 1.001 + 1e-30).all(), float((diff / (bound + 1e-30)).max())
+    return float((diff / np.maximum(np.abs(ref).max(-1, keepdims=True), 1e-30)).max())
+
+
 def test_golden_256x256_N20(cuda):
     d = golden("ptm_shared_256x256_N20.npz")
     I = np.asarray(d["I"]).astype(np.uint8)
@@ -48,8 +58,8 @@ def test_vs_oracle(cuda, basis, N, layout):
         pv = np.linalg.pinv(o.design("ptm" if basis == "ptm" else "hsh", lu, lv)[:, :k])
         for c in range(2):
             got = coef[c].reshape(P, k) if layout == "pixel" else coef[c].reshape(k, P).T
-            err, ok = coef_close(got, (pv @ I[c].astype(np.float64)).T, rtol=1e-6)
-            assert ok, (P, c, err)
+            err = q8_close(got, pv, I[c])  # the documented quantization bound, per coefficient
+            assert err <= (1e-6 if N > k else 1e-5), (P, c, err)  # N = k: a square, less well-conditioned solve
 
 
 def test_max_lights_and_extremes(cuda):
