@@ -159,15 +159,59 @@ def synth_cams(n, seed, H, W):
                      rad * np.cos(th)], -1)
 
 
+# source files that define each profiled kernel (and what it includes); the PMC traffic recorded for a kernel
+# is reported only while these files are byte-identical to the ones the counters were taken on
+KERNEL_SOURCES = {
+    "fit_shared_valu": ["rti_fit.hip"], "fit_shared_tile": ["rti_fit.hip"], "fit_shared_mfma": ["rti_fit.hip"],
+    "fit_q8": ["rti_fit_q8.hip", "rti_q8.h"], "fit_shared_residual_k": ["rti_fitres.hip"],
+    "fit_residual_k": ["rti_residual.hip"], "relight_eval": ["rti_relight.hip", "rti_convert.h"],
+    "relight_frame": ["rti_relight.hip", "rti_convert.h"], "fit_perpixel_cam": ["rti_perpixel.hip"],
+    "apply_op": ["rti_operator.hip"], "rbf_": ["rti_rbf.hip"],
+}
+COMMON_SOURCES = ["rti_internal.h", "rti_basis.h"]
+
+
+def kernel_sources(kernel_regex):
+    for root, files in KERNEL_SOURCES.items():
+        if kernel_regex.startswith(root) or root.startswith(kernel_regex):
+            return [f"smartphone-based-rti_amd/csrc/{f}" for f in files + COMMON_SOURCES]
+    return None
+
+
+def sources_sha16(files):
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_traffic(workload_key):
+    """PMC bytes per step for this workload from profiles/traffic.json, with its provenance: reported only when
+    the kernel source files the counters were taken on (entry['sources'], hashed as entry['src_sha16']) are
+    unchanged — a kernel edited since its PMC pass yields traffic None and traffic_source.stale = true."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
-            entry = json.load(f).get(workload_key) or {}
-        # per step: launch generations split one step into launches_per_step launches
-        return entry.get("traffic_bytes_per_step", entry.get("traffic_bytes_per_launch"))
+            entry = json.load(f).get(workload_key)
     except (OSError, ValueError):
-        return None
+        return None, None
+    if not entry:
+        return None, None
+    src = {"key": workload_key, "kernel": entry.get("kernel_symbol"), "commit": entry.get("commit"),
+           "src_sha16": entry.get("src_sha16")}
+    files = entry.get("sources")
+    try:
+        now = sources_sha16(files) if files else None
+    except OSError:
+        now = None
+    src["stale"] = not (files and now == entry.get("src_sha16"))
+    if src["stale"]:
+        return None, src
+    # per step: launch generations split one step into launches_per_step launches
+    return entry.get("traffic_bytes_per_step", entry.get("traffic_bytes_per_launch")), src
 
 
 def oracle():
@@ -218,13 +262,20 @@ class Workload:
         and rocprofv3's per-launch average x L is the gap-free figure)."""
         gbs = self.alg_bytes / (kernel_ms * 1e-3) / 1e9
         L = int(self.launches)
+        traffic, tsrc = self.traffic_entry()
         return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": self.traffic(), "kernel_ms": round(kernel_ms, 4),
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                "kernel_ms": round(kernel_ms, 4),
                 "alg_bytes_per_launch": self.alg_bytes / L, "alg_bytes_per_step": self.alg_bytes,
                 "launches_per_step": L, "kernel_ms_per_launch": round(kernel_ms / L, 5)}
 
     def traffic(self):
         return None
+
+    def traffic_entry(self):
+        """(PMC traffic bytes per step or None, its provenance or None)."""
+        t = self.traffic()
+        return t if isinstance(t, tuple) else (t, None)
 
 
 class FitWorkload(Workload):

@@ -10,8 +10,8 @@
 //   * a 512-thread workgroup owns a tile of R = 1024 pixels of one channel and sweeps the lights in steps
 //     of 64; per step wave w loads planes 8w..8w+7 of the tile (one 16-byte non-temporal load per lane and
 //     plane: 1 KiB per wave-instruction), flips the sign bit (x − 128) and parks them in a double-buffered
-//     LDS tile [2][64 planes][R + 16 bytes]; one barrier per step, the next step's loads issued before the
-//     current step's MFMAs;
+//     LDS tile [2][64 planes][R + 16 bytes]; one barrier per step, the loads of the next two steps in flight
+//     in registers (128 KiB per CU) while the current step's MFMAs run;
 //   * each wave then reads its 128 pixels back as MFMA B operands with ds_read_b64_tr_b8 (the hardware
 //     transpose: a lane receives 8 planes of one pixel), two reads per 16-pixel column group, and issues
 //     one MFMA per digit against the digit's A fragment (the operator, staged in LDS once per workgroup);
@@ -67,22 +67,28 @@ __device__ __forceinline__ void q8_store(float* __restrict__ dst, int64_t P, int
 template <int K, int LAYOUT>
 __global__ void __launch_bounds__(64 * Q8_W)
 fit_q8(const unsigned char* __restrict__ op, int N, const unsigned char* __restrict__ I, int64_t pb, int64_t pe,
-       int64_t P, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+       int tpw, int64_t P, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int T = q8_steps(N);
-  unsigned char* __restrict__ lfrag = lds;                      // [T][4][64][16]
-  unsigned char* __restrict__ tile = lds + q8_frag_bytes(N);    // [2][64][RS]
-  for (int i = threadIdx.x; i < T * Q8_DIGITS * 64; i += 64 * Q8_W)
+  // the whole operator (A fragments [T][4][64][16], scales, corrections) is staged in LDS once: the stream
+  // loop then issues no global loads but the stack's, so its counted vmcnt waits only ever wait for stack bytes
+  unsigned char* __restrict__ lfrag = lds;                          // [T][4][64][16] + scale[16] + corr[16][4]
+  unsigned char* __restrict__ tile = lds + q8_operator_bytes(N);    // [2][64][RS]
+  for (int i = threadIdx.x; i < (int)(q8_operator_bytes(N) / 16); i += 64 * Q8_W)
     *reinterpret_cast<v4i*>(lfrag + 16 * i) = *reinterpret_cast<const v4i*>(op + 16 * i);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t t0 = pb + (int64_t)blockIdx.x * Q8_R;
+  // this workgroup's tiles: tpw consecutive 1024-pixel tiles from tb0, streamed as S = ntiles·T steps of 64
+  // lights through one pipeline, so only the first step of the first tile waits for HBM cold
+  const int64_t tb0 = pb + (int64_t)blockIdx.x * tpw * Q8_R;
+  const int ntiles = (int)min((int64_t)tpw, (pe - tb0 + Q8_R - 1) / Q8_R);
+  const int S = ntiles * T;
   const unsigned char* __restrict__ src = I + (int64_t)blockIdx.y * cstride;
-  int64_t px = t0 + 16 * lane;
-  px = px < pe ? px : pe - 16;  // lanes past the image re-read its last 16 pixels (never stored)
 
-  v4i st[8];
-  auto load = [&](int t) {
+  auto load = [&](int s, v4i (&st)[8]) {
+    const int ti = s / T, t = s - ti * T;
+    int64_t px = tb0 + (int64_t)ti * Q8_R + 16 * lane;
+    px = px < pe ? px : pe - 16;  // lanes past the image re-read its last 16 pixels (never stored)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       int n = t * Q8_STEP + 8 * wave + j;
@@ -90,17 +96,20 @@ fit_q8(const unsigned char* __restrict__ op, int N, const unsigned char* __restr
       st[j] = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(src + (int64_t)n * lstride + px));
     }
   };
-  auto park = [&](int b) {
+  auto park = [&](int b, const v4i (&st)[8]) {
     unsigned char* tb = tile + b * (Q8_STEP * Q8_RS) + (8 * wave) * Q8_RS + 16 * lane;
 #pragma unroll
     for (int j = 0; j < 8; ++j) *reinterpret_cast<v4i*>(tb + j * Q8_RS) = st[j] ^ (int)0x80808080;
   };
 
   v4i acc[Q8_G][Q8_DIGITS];
+  auto zero = [&]() {
 #pragma unroll
-  for (int c = 0; c < Q8_G; ++c)
+    for (int c = 0; c < Q8_G; ++c)
 #pragma unroll
-    for (int d = 0; d < Q8_DIGITS; ++d) acc[c][d] = v4i{0, 0, 0, 0};
+      for (int d = 0; d < Q8_DIGITS; ++d) acc[c][d] = v4i{0, 0, 0, 0};
+  };
+  zero();
 
   // transposed-read address of this lane: group g reads rows 8g + q (and 32 + 8g + q), q = (lane & 15) >> 1,
   // bytes 8·(lane & 1) of each 16-pixel column group
@@ -121,44 +130,67 @@ fit_q8(const unsigned char* __restrict__ op, int N, const unsigned char* __restr
     }
   };
 
-  load(0);
-  park(0);
+  // per-row scale and sign-flip corrections of the coefficients (rows 4g .. 4g+3 for this lane), read per
+  // tile from the LDS copy of the operator rather than held in registers across the stream
+  const double* scale = reinterpret_cast<const double*>(lfrag + q8_frag_bytes(N));
+  const int* corr = reinterpret_cast<const int*>(scale + 16);
+  float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
+  // acc[c][d][r] = digit d's sum for coefficient 4g + r of pixel t0 + 128·wave + 16c + (lane & 15); the stores
+  // of tile i are issued while the loads of tile i + 1 are in flight
+  auto finish = [&](int ti) {
+    const int64_t t0 = tb0 + (int64_t)ti * Q8_R;
+    if (4 * g < K) {
+      double sc[4];
+      int cr[4][Q8_DIGITS];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sc[r] = scale[4 * g + r];
+#pragma unroll
+        for (int d = 0; d < Q8_DIGITS; ++d) cr[r][d] = corr[(4 * g + r) * Q8_DIGITS + d];
+      }
+#pragma unroll
+      for (int c = 0; c < Q8_G; ++c) {
+        const int64_t p = t0 + Q8_WPX * wave + 16 * c + (lane & 15);
+        if (p >= pe) continue;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double sm = (double)(acc[c][0][r] + cr[r][0]);  // exact: |Σ| < 2^53 for N < 2^18
+#pragma unroll
+          for (int d = 1; d < Q8_DIGITS; ++d) sm = fma(sm, 128.0, (double)(acc[c][d][r] + cr[r][d]));
+          v[r] = (float)(sm * sc[r]);
+        }
+        q8_store<K, LAYOUT>(dst, P, p, g, v);
+      }
+    }
+    zero();
+  };
+  // The stream loop keeps every vector-memory operation unconditional or in a fixed place, so the compiler's
+  // counted vmcnt waits stay exact (a load or store on one branch of a loop makes it wait conservatively,
+  // which here drained the prefetch every step): loads of steps past the end re-read step S − 1, an odd
+  // stream gets one dummy step that is parked but not computed, and a finished tile's stores are issued at
+  // the start of the next step, before that step's loads, so waiting for the older step never waits for
+  // the newer one.  Two steps of loads in flight (128 KiB per CU): sb holds step s + 1 (loaded during step
+  // s − 1), sa receives step s + 2; the roles swap every step.
+  v4i sa[8], sb[8];
+  load(0, sa);
+  load(S > 1 ? 1 : 0, sb);
+  park(0, sa);
   __syncthreads();
-  for (int t = 0; t < T; ++t) {
-    const bool more = t + 1 < T;  // workgroup-uniform
-    if (more) load(t + 1);
-    compute(t & 1, t);
-    if (more) park((t + 1) & 1);
+  const int S2 = S + (S & 1);
+  for (int s = 0; s < S2; s += 2) {
+    if (s > 0 && s % T == 0) finish(s / T - 1);
+    load(min(s + 2, S - 1), sa);
+    compute(0, s % T);
+    park(1, sb);
+    __syncthreads();
+    if (s + 1 < S && (s + 1) % T == 0) finish((s + 1) / T - 1);
+    load(min(s + 3, S - 1), sb);
+    if (s + 1 < S) compute(1, (s + 1) % T);
+    park(0, sa);
     __syncthreads();
   }
-
-  // acc[c][d][r] = digit d's sum for coefficient 4g + r of pixel t0 + 128·wave + 16c + (lane & 15)
-  const double* scale = reinterpret_cast<const double*>(op + q8_frag_bytes(N));
-  const int* corr = reinterpret_cast<const int*>(scale + 16);
-  if (4 * g >= K) return;
-  double sc[4];
-  int cr[4][Q8_DIGITS];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    sc[r] = scale[4 * g + r];
-#pragma unroll
-    for (int d = 0; d < Q8_DIGITS; ++d) cr[r][d] = corr[(4 * g + r) * Q8_DIGITS + d];
-  }
-  float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
-#pragma unroll
-  for (int c = 0; c < Q8_G; ++c) {
-    const int64_t p = t0 + Q8_WPX * wave + 16 * c + (lane & 15);
-    if (p >= pe) continue;
-    float v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      double s = (double)(acc[c][0][r] + cr[r][0]);  // exact: |Σ| < 2^53 for N < 2^18
-#pragma unroll
-      for (int d = 1; d < Q8_DIGITS; ++d) s = fma(s, 128.0, (double)(acc[c][d][r] + cr[r][d]));
-      v[r] = (float)(s * sc[r]);
-    }
-    q8_store<K, LAYOUT>(dst, P, p, g, v);
-  }
+  finish(ntiles - 1);
 }
 
 struct Q8Args {
@@ -172,9 +204,10 @@ struct Q8Args {
   int64_t ocstride;
   hipStream_t s;
   int64_t pb = 0, pe = 0;
+  int tpw = 1;  // consecutive tiles streamed by one workgroup
 };
 
-size_t q8_lds_bytes(int N) { return (size_t)q8_frag_bytes(N) + (size_t)2 * Q8_STEP * Q8_RS; }
+size_t q8_lds_bytes(int N) { return (size_t)q8_operator_bytes(N) + (size_t)2 * Q8_STEP * Q8_RS; }
 
 template <int K, int LAYOUT>
 int launch_q8_t(const Q8Args& a) {
@@ -184,8 +217,10 @@ int launch_q8_t(const Q8Args& a) {
                           (int)lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_q8: cannot reserve %zu B of LDS", lds);
   const int64_t pe = a.pe ? a.pe : a.P;
-  const dim3 grid(grid_1d(pe - a.pb, Q8_R), a.C);
-  hipLaunchKernelGGL(kern, grid, dim3(64 * Q8_W), lds, a.s, a.op, a.N, a.I, a.pb, pe, a.P, a.lstride, a.cstride,
+  const int64_t tiles = (pe - a.pb + Q8_R - 1) / Q8_R;
+  const int tpw = a.tpw > 0 ? a.tpw : 1;
+  const dim3 grid((unsigned)((tiles + tpw - 1) / tpw), a.C);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * Q8_W), lds, a.s, a.op, a.N, a.I, a.pb, pe, tpw, a.P, a.lstride, a.cstride,
                      a.coef, a.ocstride);
   return check_launch("rti_fit_shared_q8");
 }
@@ -246,38 +281,13 @@ extern "C" int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I,
       !aligned_to(coef, 16) || a.ocstride % 4)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_q8: needs P, strides and pointers 16-byte aligned");
   note_launches(1);
-  // launch generations (rti_fit.hip §4.0): one 1024-pixel workgroup per CU, so a launch of at most 4 rounds
-  // of workgroups per channel with the last round >= 85 % full keeps the chip's waves sweeping in step
-  int parts = 1;
-  const int64_t tpc = (P + Q8_R - 1) / Q8_R, cus = device_cus(), cap = 4 * cus;
-  if (!(kernel & RTI_KERNEL_ONE_LAUNCH) && tpc * C > cap) {
-    const int p0 = (int)((tpc + cap - 1) / cap);
-    parts = p0;
-    for (int p = p0; p < p0 + 4; ++p) {
-      const int64_t per = (tpc + p - 1) / p, last = per % cus;
-      if (last == 0 || last * 100 >= cus * 85) {
-        parts = p;
-        break;
-      }
-    }
-  }
-  if (parts == 1 && (kernel & RTI_KERNEL_ONE_LAUNCH)) return launch_q8(a);
-  if (parts == 1 && tpc * C <= cap) return launch_q8(a);
-  const int64_t per = (tpc + parts - 1) / parts;
-  int launches = 0;
-  for (int c = 0; c < C; ++c) {
-    Q8Args b = a;
-    b.C = 1;
-    b.I = a.I + (size_t)c * a.cstride;
-    b.coef = a.coef + (size_t)c * a.ocstride;
-    for (int i = 0; i < parts; ++i) {
-      b.pb = i * per * Q8_R;
-      b.pe = (i + 1) * per * Q8_R < P ? (i + 1) * per * Q8_R : P;
-      if (b.pb >= b.pe) break;
-      const int st = launch_q8(b);
-      if (st != RTI_OK) return st;
-      note_launches(++launches);
-    }
-  }
-  return RTI_OK;
+  // One workgroup per CU (146 KiB of LDS), every workgroup streaming tpw consecutive tiles through its load
+  // pipeline: a tile of 1024 pixels x N <= 448 lights is only 2-7 steps, and started cold each tile would
+  // wait for HBM once.  AUTO: one launch over the channels, tpw = ceil(tiles per channel / workgroups per
+  // channel) with about one workgroup per CU; RTI_KERNEL_CHUNKS(n) sets tpw = n (measurement).
+  const int64_t tpc = (P + Q8_R - 1) / Q8_R, cus = device_cus();
+  const int want = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  const int64_t wpc = (cus + C - 1) / C;  // workgroups per channel
+  a.tpw = want ? want : (int)((tpc + wpc - 1) / wpc);
+  return launch_q8(a);
 }

@@ -10,7 +10,7 @@
 // full-rank A that is the same least-squares solution the SVD returns (the
 // fp64 normal equations lose cond(A)²·1e-16); a pixel whose Cholesky pivots
 // show an ill-conditioned A (ne_solve) is marked and re-solved by a second,
-// refine launch (qr_refine_*) with a streaming fp64 Givens QR of A itself
+// refine launch (refine_*) with a streaming fp64 Givens QR of A itself
 // (qr_solve), which loses cond(A)·1e-16 like the reference's SVD; a
 // rank-deficient A gives NaN coefficients, as the reference's division by a
 // zero singular value does.
@@ -195,10 +195,17 @@ __device__ __forceinline__ void qr_solve(int N, double rcond, Row row, double (&
       const double xj = x[j];
       if (xj == 0.0) continue;
       const double rjj = R[tri(j, j)];
-      const double m = fmax(fabs(rjj), fabs(xj));  // scaled hypot: no overflow/underflow
-      const double h = m * sqrt((rjj / m) * (rjj / m) + (xj / m) * (xj / m));
-      const double c = rjj / h, sn = xj / h;
-      R[tri(j, j)] = h;
+      // h = hypot(rjj, xj) and 1/h from v_rsq_f64 + two Newton steps (≈1 ulp, tools/probe/rsq_probe.hip):
+      // the rotation stays orthogonal to ~1e-16, so the QR keeps its backward stability, at a third of the
+      // latency of IEEE sqrt + divides (the refine lane runs its N lights serially).  Intensities and PTM
+      // rows are O(1e3) at most: h² neither overflows nor underflows.
+      const double h2 = fma(rjj, rjj, xj * xj);
+      double y = __builtin_amdgcn_rsq(h2);
+      const double hh = 0.5 * h2;
+      y = fma(y, fma(-hh * y, y, 0.5), y);
+      y = fma(y, fma(-hh * y, y, 0.5), y);
+      const double c = rjj * y, sn = xj * y;
+      R[tri(j, j)] = h2 * y;
 #pragma unroll
       for (int k = j + 1; k < 6; ++k) {
         const double t = R[tri(j, k)];
@@ -249,20 +256,22 @@ __device__ __forceinline__ void store_coef(TC* __restrict__ coef, int64_t P, int
   }
 }
 
-// A pixel the normal equations cannot take leaves this signalling-NaN bit pattern in its first
-// coefficient for the refine pass (qr_refine_*), which re-solves exactly those pixels by Givens QR.
-// No arithmetic produces it (results are quiet NaNs), and the refine pass overwrites every instance.
+// A pixel the fast kernel cannot finish leaves one of two signalling-NaN bit patterns in its first
+// coefficient for the refine pass (refine_*): EXACT = a light vector the fast form could not round with
+// certainty (redo the pixel with the IEEE light vectors), QR = an ill-conditioned system (redo it by Givens
+// QR).  No arithmetic produces these patterns (results are quiet NaNs), and the refine pass overwrites them.
+constexpr int MARK_NONE = 0, MARK_EXACT = 1, MARK_QR = 2;
 template <typename TC>
-struct QrMark;
+struct Mark;
 template <>
-struct QrMark<double> {
+struct Mark<double> {
   using U = unsigned long long;
-  static constexpr U bits = 0x7FF0515249514D4Bull;
+  static constexpr U exact = 0x7FF0515249514D45ull, qr = 0x7FF0515249514D4Bull;
 };
 template <>
-struct QrMark<float> {
+struct Mark<float> {
   using U = unsigned int;
-  static constexpr U bits = 0x7FA51A11u;
+  static constexpr U exact = 0x7FA51A10u, qr = 0x7FA51A11u;
 };
 
 template <typename TC, int LAYOUT>
@@ -273,18 +282,18 @@ __device__ __forceinline__ TC* coef0(TC* coef, int64_t P, int64_t p) {
 
 template <typename TC, int LAYOUT>
 __device__ __forceinline__ void solve_store(const Normal6& ne, double rcond, TC* __restrict__ coef, int64_t P,
-                                            int64_t p, bool redo = false) {
+                                            int64_t p, bool inexact_dirs = false) {
   double a[6];
-  const bool ill = ne_solve(ne, rcond, a) || redo;
+  const bool ill = ne_solve(ne, rcond, a);
   store_coef<TC, LAYOUT>(coef, P, p, a);
-  if (__builtin_expect(ill, 0))
-    *reinterpret_cast<typename QrMark<TC>::U*>(coef0<TC, LAYOUT>(coef, P, p)) = QrMark<TC>::bits;
+  if (__builtin_expect(ill || inexact_dirs, 0))
+    *reinterpret_cast<typename Mark<TC>::U*>(coef0<TC, LAYOUT>(coef, P, p)) = ill ? Mark<TC>::qr : Mark<TC>::exact;
 }
 
 template <typename TC, int LAYOUT>
-__device__ __forceinline__ bool qr_marked(const TC* coef, int64_t P, int64_t p) {
-  return *reinterpret_cast<const typename QrMark<TC>::U*>(coef0<TC, LAYOUT>(const_cast<TC*>(coef), P, p)) ==
-         QrMark<TC>::bits;
+__device__ __forceinline__ int mark_of(const TC* coef, int64_t P, int64_t p) {
+  const auto u = *reinterpret_cast<const typename Mark<TC>::U*>(coef0<TC, LAYOUT>(const_cast<TC*>(coef), P, p));
+  return u == Mark<TC>::exact ? MARK_EXACT : (u == Mark<TC>::qr ? MARK_QR : MARK_NONE);
 }
 
 template <typename T, typename TC, int LAYOUT>
@@ -311,26 +320,42 @@ fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I
   solve_store<TC, LAYOUT>(ne, rcond, coef, P, p, chk.ambiguous());
 }
 
-// Refine pass of fit_perpixel_cam: the marked pixels (ill-conditioned, or a light vector the fast form
-// could not round with certainty) with exact light vectors and Givens QR (qr_solve).  A scan of
-// one coefficient per pixel when nothing is marked (8 B per pixel against the fit's 4·N).
+// Refine pass of fit_perpixel_cam, one lane per marked pixel: EXACT pixels are re-accumulated with the
+// IEEE light vectors (light_dir_exact) and solved as in the fit (falling through to QR if ill-conditioned),
+// QR pixels go straight to the Givens QR of their exact rows.  A scan of one coefficient per pixel when
+// nothing is marked; a marked lane runs its N lights serially (tens of µs at N = 100).
 template <typename T, typename TC, int LAYOUT>
 __global__ void __launch_bounds__(256)
-qr_refine_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
-              double x0, double y0, double rcond, TC* __restrict__ coef) {
+refine_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
+           double x0, double y0, double rcond, TC* __restrict__ coef) {
   const int64_t P = (int64_t)H * W;
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= P || !qr_marked<TC, LAYOUT>(coef, P, p)) return;
+  if (p >= P) return;
+  const int mark = mark_of<TC, LAYOUT>(coef, P, p);
+  if (mark == MARK_NONE) return;
   const double px = x0 + (double)(p % W);
   const double py = y0 + (double)(p / W);
   const T* __restrict__ src = I + p;
   double a[6];
-  qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
-    float lu, lv;
-    light_dir_exact(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv);
-    ptm_row_d(lu, lv, r);
-    L = ld_d(src + (int64_t)n * lstride);
-  }, a);
+  bool qr = mark == MARK_QR;
+  if (!qr) {
+    Normal6 ne;
+    ne_zero(ne);
+    for (int n = 0; n < N; ++n) {
+      float lu, lv;
+      light_dir_exact(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv);
+      ne_add(ne, lu, lv, ld_d(src + (int64_t)n * lstride));
+    }
+    ne_finish(ne, N);
+    qr = ne_solve(ne, rcond, a);
+  }
+  if (qr)
+    qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
+      float lu, lv;
+      light_dir_exact(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv);
+      ptm_row_d(lu, lv, r);
+      L = ld_d(src + (int64_t)n * lstride);
+    }, a);
   store_coef<TC, LAYOUT>(coef, P, p, a);
 }
 
@@ -351,10 +376,10 @@ fit_perpixel_dirs(const float* __restrict__ lu, const float* __restrict__ lv, co
 
 template <typename T, typename TC, int LAYOUT>
 __global__ void __launch_bounds__(256)
-qr_refine_dirs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N,
+refine_dirs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N,
                int64_t P, double rcond, TC* __restrict__ coef) {
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= P || !qr_marked<TC, LAYOUT>(coef, P, p)) return;
+  if (p >= P || mark_of<TC, LAYOUT>(coef, P, p) != MARK_QR) return;
   const int64_t base = p * N;
   double a[6];
   qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
@@ -391,7 +416,7 @@ void launch_cam(const double* cams, int N, const void* I, int H, int W, int64_t 
   const int64_t P = (int64_t)H * W;
   hipLaunchKernelGGL((fit_perpixel_cam<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N,
                      static_cast<const T*>(I), H, W, ls, x0, y0, rcond, static_cast<TC*>(coef));
-  hipLaunchKernelGGL((qr_refine_cam<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N,
+  hipLaunchKernelGGL((refine_cam<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N,
                      static_cast<const T*>(I), H, W, ls, x0, y0, rcond, static_cast<TC*>(coef));
 }
 
@@ -418,7 +443,7 @@ void launch_dirs(const float* lu, const float* lv, const void* I, int N, int64_t
                  hipStream_t s) {
   hipLaunchKernelGGL((fit_perpixel_dirs<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, lu, lv,
                      static_cast<const T*>(I), N, P, rcond, static_cast<TC*>(coef));
-  hipLaunchKernelGGL((qr_refine_dirs<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, lu, lv,
+  hipLaunchKernelGGL((refine_dirs<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, lu, lv,
                      static_cast<const T*>(I), N, P, rcond, static_cast<TC*>(coef));
 }
 

@@ -97,28 +97,28 @@ def test_q8_matches_fp32_stream_and_is_used(cuda):
     assert ea <= 1e-6 and ea <= eb
 
 
-def test_launch_generations_bit_identical(cuda):
-    """AUTO splits a large q8 fit into launches over pixel ranges of whole 1024-pixel tiles; the result
-    equals RTI_KERNEL_ONE_LAUNCH's bit for bit (ragged P, 3 channels, HSH-16)."""
-    N, C, P = 200, 3, 1024 * 2100 + 16 * 5
-    lu, lv = o.synth_dirs(N, 4)
-    pv = o.pinv_shared("hsh", lu, lv)
-    op = torch.as_tensor(rti.q8_operator(pv), device=cuda)
-    g = torch.Generator(device=cuda).manual_seed(5)
-    I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda, dtype=torch.uint8)
-    outs = []
-    for flags in (0, L.RTI_KERNEL_ONE_LAUNCH):
-        coef = torch.full((C, P, 16), float("nan"), device=cuda)
-        rti.api.fit_q8_into(op, I, coef, k=16, flags=flags)
-        outs.append((coef, int(L.lib().rti_last_launch_count())))
-    (a, la), (b, lb) = outs
-    assert la > 1 and lb == 1, (la, lb)
-    assert not torch.isnan(a).any() and torch.equal(a, b)
-    idx = torch.as_tensor(np.unique(np.r_[np.random.default_rng(1).integers(0, P, 512), 0, P - 1]), device=cuda)
-    for c in range(C):
-        ref = (pv @ I[c][:, idx].double().cpu().numpy()).T
-        err, ok = coef_close(a[c][idx].cpu().numpy(), ref, rtol=1e-6)
-        assert ok, (c, err)
+def test_tile_streams_bit_identical(cuda):
+    """AUTO lets every workgroup stream several consecutive 1024-pixel tiles through one load pipeline; the
+    result equals one cold tile per workgroup (RTI_KERNEL_CHUNKS(1)) and 3 tiles per workgroup bit for bit
+    (ragged P: a partial last tile and a short last stream, 3 channels, HSH-16 and PTM-6)."""
+    for k, N in ((16, 200), (6, 100)):
+        C, P = 3, 1024 * 2100 + 16 * 5
+        lu, lv = o.synth_dirs(N, 4)
+        pv = o.pinv_shared("hsh" if k == 16 else "ptm", lu, lv)
+        op = torch.as_tensor(rti.q8_operator(pv), device=cuda)
+        g = torch.Generator(device=cuda).manual_seed(5)
+        I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda, dtype=torch.uint8)
+        outs = []
+        for flags in (0, 1 << L.RTI_KERNEL_CHUNKS_SHIFT, 3 << L.RTI_KERNEL_CHUNKS_SHIFT):
+            coef = torch.full((C, P, k), float("nan"), device=cuda)
+            rti.api.fit_q8_into(op, I, coef, k=k, flags=flags)
+            outs.append(coef)
+        a = outs[0]
+        assert not torch.isnan(a).any() and torch.equal(a, outs[1]) and torch.equal(a, outs[2])
+        idx = torch.as_tensor(np.unique(np.r_[np.random.default_rng(1).integers(0, P, 512), 0, P - 1]), device=cuda)
+        for c in range(C):
+            err = q8_close(a[c][idx].cpu().numpy(), pv, I[c][:, idx].cpu().numpy())
+            assert err <= 1e-6, (k, c, err)
 
 
 def test_fallbacks_keep_reference_semantics(cuda):

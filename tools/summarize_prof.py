@@ -9,11 +9,16 @@ units are KiB: ×1024).
         --key WORKLOAD --alg-bytes B (per bench step) [--launches-per-step L] [--out profiles/traffic.json]
 """
 import argparse
+import collections
 import csv
 import glob
 import json
 import os
 import re
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402  (kernel_sources / sources_sha16: the provenance bench.py checks)
 
 
 def rows(d, suffix):
@@ -41,11 +46,19 @@ def main():
     summary = {"kernel_regex": args.kernel, "alg_bytes_per_launch": args.alg_bytes / L, "launches_per_step": L,
                "alg_bytes_per_step": args.alg_bytes}
     if args.trace:
-        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows(args.trace, "kernel_trace.csv")
-                if rx.search(r["Kernel_Name"])]
+        trace = [r for r in rows(args.trace, "kernel_trace.csv") if rx.search(r["Kernel_Name"])]
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace]
         if durs:
             summary["launches"] = len(durs)
             summary["avg_duration_ns"] = sum(durs) / len(durs)
+            # provenance (bench.py load_traffic): the profiled kernel's symbol (most launches) and a hash of the
+            # source files that define it; bench reports this traffic only while those files are unchanged
+            names = collections.Counter(r["Kernel_Name"] for r in trace)
+            summary["kernel_symbol"] = names.most_common(1)[0][0]
+    files = bench.kernel_sources(args.kernel)
+    if files:
+        summary["sources"] = files
+        summary["src_sha16"] = bench.sources_sha16(files)
     for name, d, corr in (("FETCH_SIZE", args.fetch, 2.0), ("WRITE_SIZE", args.write, 1.0)):
         if not d:
             continue
