@@ -78,16 +78,21 @@ fit_q8(const unsigned char* __restrict__ op, int N, const unsigned char* __restr
     *reinterpret_cast<v4i*>(lfrag + 16 * i) = *reinterpret_cast<const v4i*>(op + 16 * i);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // this workgroup's tiles: tpw consecutive 1024-pixel tiles from tb0, streamed as S = ntiles·T steps of 64
-  // lights through one pipeline, so only the first step of the first tile waits for HBM cold
-  const int64_t tb0 = pb + (int64_t)blockIdx.x * tpw * Q8_R;
-  const int ntiles = (int)min((int64_t)tpw, (pe - tb0 + Q8_R - 1) / Q8_R);
+  // this workgroup's tiles: tiles blockIdx.x, blockIdx.x + G, blockIdx.x + 2G, ... (G = gridDim.x) of the
+  // [pb, pe) range, at most tpw of them, streamed as S = ntiles·T steps of 64 lights through one pipeline (only
+  // the first step waits for HBM cold).  Interleaved, not consecutive, tiles: the workgroups sweep the planes
+  // in step, so at any moment the chip reads one contiguous G-tile slab of each plane (c4 u8
+  // 1.91 ms with each workgroup on its own consecutive run of tiles)
+  const int64_t ntot = (pe - pb + Q8_R - 1) / Q8_R;
+  const int G = gridDim.x;
+  const int ntiles = (int)min((int64_t)tpw, (ntot - blockIdx.x + G - 1) / G);
   const int S = ntiles * T;
+  auto tile_px = [&](int ti) { return pb + ((int64_t)ti * G + blockIdx.x) * Q8_R; };
   const unsigned char* __restrict__ src = I + (int64_t)blockIdx.y * cstride;
 
   auto load = [&](int s, v4i (&st)[8]) {
     const int ti = s / T, t = s - ti * T;
-    int64_t px = tb0 + (int64_t)ti * Q8_R + 16 * lane;
+    int64_t px = tile_px(ti) + 16 * lane;
     px = px < pe ? px : pe - 16;  // lanes past the image re-read its last 16 pixels (never stored)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -138,7 +143,7 @@ fit_q8(const unsigned char* __restrict__ op, int N, const unsigned char* __restr
   // acc[c][d][r] = digit d's sum for coefficient 4g + r of pixel t0 + 128·wave + 16c + (lane & 15); the stores
   // of tile i are issued while the loads of tile i + 1 are in flight
   auto finish = [&](int ti) {
-    const int64_t t0 = tb0 + (int64_t)ti * Q8_R;
+    const int64_t t0 = tile_px(ti);
     if (4 * g < K) {
       double sc[4];
       int cr[4][Q8_DIGITS];
@@ -219,7 +224,7 @@ int launch_q8_t(const Q8Args& a) {
   const int64_t pe = a.pe ? a.pe : a.P;
   const int64_t tiles = (pe - a.pb + Q8_R - 1) / Q8_R;
   const int tpw = a.tpw > 0 ? a.tpw : 1;
-  const dim3 grid((unsigned)((tiles + tpw - 1) / tpw), a.C);
+  const dim3 grid((unsigned)((tiles + tpw - 1) / tpw), a.C);  // workgroup w streams tiles w, w + G, ...
   hipLaunchKernelGGL(kern, grid, dim3(64 * Q8_W), lds, a.s, a.op, a.N, a.I, a.pb, pe, tpw, a.P, a.lstride, a.cstride,
                      a.coef, a.ocstride);
   return check_launch("rti_fit_shared_q8");
@@ -281,13 +286,13 @@ extern "C" int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I,
       !aligned_to(coef, 16) || a.ocstride % 4)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_q8: needs P, strides and pointers 16-byte aligned");
   note_launches(1);
-  // One workgroup per CU (146 KiB of LDS), every workgroup streaming tpw consecutive tiles through its load
-  // pipeline: a tile of 1024 pixels x N <= 448 lights is only 2-7 steps, and started cold each tile would
-  // wait for HBM once.  AUTO: one launch over the channels, tpw = ceil(tiles per channel / workgroups per
+  // One workgroup per CU (146 KiB of LDS), every workgroup streaming tpw tiles (interleaved with the other
+  // workgroups') through its load pipeline: a tile of 1024 pixels x N <= 448 lights is only 2-7 steps, and
+  // started cold each tile would wait for HBM once.  AUTO: one launch over the channels, tpw = ceil(tiles per channel / workgroups per
   // channel) with about one workgroup per CU; RTI_KERNEL_CHUNKS(n) sets tpw = n (measurement).
   const int64_t tpc = (P + Q8_R - 1) / Q8_R, cus = device_cus();
   const int want = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
-  const int64_t wpc = (cus + C - 1) / C;  // workgroups per channel
+  const int64_t wpc = cus >= C ? cus / C : 1;  // workgroups per channel: at most one per CU over all channels
   a.tpw = want ? want : (int)((tpc + wpc - 1) / wpc);
   return launch_q8(a);
 }

@@ -76,10 +76,13 @@ __device__ __forceinline__ void ne_finish(Normal6& ne, int N) { ne.m[tri(5, 5)] 
 // at the low 29 bits of q's fp64 significand, so fp32(q̃) == fp32(q) unless q̃ lies within those few
 // ulps of an fp32 rounding midpoint (low 29 bits = 2^28), or the fp32 result is subnormal.  The fast form
 // folds both tests into two running minima (mid_key == 0, or |l| < FLT_MIN, flags the light: ≈1 in
-// 4·10⁶ components), and a flagged pixel is re-solved by the refine pass, whose light_dir_exact uses the
+// 1.7·10⁷ components), and a flagged pixel is re-solved by the refine pass, whose light_dir_exact uses the
 // IEEE sqrt and divide of rti_light_dirs.  Pinned by tests/golden/ptm_perpixel_32x32_N50.npz through
 // rti_fit_perpixel_cam (test_gpu_perpixel_relight.py); the ulp budget by tools/probe/rsq_probe.hip.
-constexpr uint32_t MID_MARGIN = 64;  // fp64 ulps: the Newton-refined quotient is within a few of IEEE's
+// fp64 ulps of q: |q̃ − q_ref| <= ~4.5 ulps (s: two fma roundings vs the reference's four, <= 4 ulps of s
+// -> 2 of 1/√s; rsq + 2 Newton steps 0.99 ulp, tools/probe/rsq_probe.hip; the product 0.5; the
+// reference's sqrt and divide 0.5 each), so a margin of 16 leaves a factor 3.5
+constexpr uint32_t MID_MARGIN = 16;
 constexpr int NEWTON = 2;
 
 // 0 iff the low 29 significand bits of q lie within MID_MARGIN of 2^28 (an fp32 rounding midpoint)
@@ -281,13 +284,25 @@ __device__ __forceinline__ TC* coef0(TC* coef, int64_t P, int64_t p) {
 }
 
 template <typename TC, int LAYOUT>
+__device__ __forceinline__ void put_mark(TC* coef, int64_t P, int64_t p, int mark) {
+  *reinterpret_cast<typename Mark<TC>::U*>(coef0<TC, LAYOUT>(coef, P, p)) =
+      mark == MARK_QR ? Mark<TC>::qr : Mark<TC>::exact;
+}
+
+// Solve and store one pixel; a pixel the fast path cannot finish is marked, and so is the first pixel of its
+// wave (MARK_EXACT: "redo this pixel from the start"), so the refine pass reads one coefficient per wave
+// (64 pixels) instead of one per pixel and looks at the wave's pixels only when that one is marked.
+template <typename TC, int LAYOUT>
 __device__ __forceinline__ void solve_store(const Normal6& ne, double rcond, TC* __restrict__ coef, int64_t P,
                                             int64_t p, bool inexact_dirs = false) {
   double a[6];
   const bool ill = ne_solve(ne, rcond, a);
+  const bool marked = ill || inexact_dirs;
+  // lane 0 = the wave's first pixel (launches of 256-thread blocks): it carries the wave's flag
+  const bool any = __ballot(marked) != 0;  // every active lane takes part (not under a lane-dependent branch)
+  const bool flag = (threadIdx.x & 63) == 0 && any;
   store_coef<TC, LAYOUT>(coef, P, p, a);
-  if (__builtin_expect(ill || inexact_dirs, 0))
-    *reinterpret_cast<typename Mark<TC>::U*>(coef0<TC, LAYOUT>(coef, P, p)) = ill ? Mark<TC>::qr : Mark<TC>::exact;
+  if (__builtin_expect(marked || flag, 0)) put_mark<TC, LAYOUT>(coef, P, p, ill && !flag ? MARK_QR : MARK_EXACT);
 }
 
 template <typename TC, int LAYOUT>
@@ -298,6 +313,7 @@ __device__ __forceinline__ int mark_of(const TC* coef, int64_t P, int64_t p) {
 
 template <typename T, typename TC, int LAYOUT>
 __global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(6)))
 fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
                  double x0, double y0, double rcond, TC* __restrict__ coef) {
   const int64_t P = (int64_t)H * W;
@@ -320,6 +336,13 @@ fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I
   solve_store<TC, LAYOUT>(ne, rcond, coef, P, p, chk.ambiguous());
 }
 
+// Refine launches: 256-thread blocks, one block per 4 fit waves (256 pixels), the same pixel per lane as the
+// fit; -1 past the image.  A wave whose first pixel carries no mark has nothing to redo.
+__device__ __forceinline__ int64_t refine_pixel(int64_t P) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  return p < P ? p : -1;
+}
+
 // Refine pass of fit_perpixel_cam, one lane per marked pixel: EXACT pixels are re-accumulated with the
 // IEEE light vectors (light_dir_exact) and solved as in the fit (falling through to QR if ill-conditioned),
 // QR pixels go straight to the Givens QR of their exact rows.  A scan of one coefficient per pixel when
@@ -329,8 +352,8 @@ __global__ void __launch_bounds__(256)
 refine_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
            double x0, double y0, double rcond, TC* __restrict__ coef) {
   const int64_t P = (int64_t)H * W;
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= P) return;
+  const int64_t p = refine_pixel(P);
+  if (p < 0 || mark_of<TC, LAYOUT>(coef, P, p & ~(int64_t)63) == MARK_NONE) return;  // the wave's flag
   const int mark = mark_of<TC, LAYOUT>(coef, P, p);
   if (mark == MARK_NONE) return;
   const double px = x0 + (double)(p % W);
@@ -378,14 +401,25 @@ template <typename T, typename TC, int LAYOUT>
 __global__ void __launch_bounds__(256)
 refine_dirs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N,
                int64_t P, double rcond, TC* __restrict__ coef) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= P || mark_of<TC, LAYOUT>(coef, P, p) != MARK_QR) return;
+  const int64_t p = refine_pixel(P);
+  if (p < 0 || mark_of<TC, LAYOUT>(coef, P, p & ~(int64_t)63) == MARK_NONE) return;  // the wave's flag
+  const int mark = mark_of<TC, LAYOUT>(coef, P, p);
+  if (mark == MARK_NONE) return;
   const int64_t base = p * N;
   double a[6];
-  qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
-    ptm_row_d(lu[base + n], lv[base + n], r);
-    L = ld_d(I + base + n);
-  }, a);
+  bool qr = mark == MARK_QR;
+  if (!qr) {  // the wave's first pixel (or a pixel redone from the start): the fit's own normal equations
+    Normal6 ne;
+    ne_zero(ne);
+    for (int n = 0; n < N; ++n) ne_add(ne, lu[base + n], lv[base + n], ld_d(I + base + n));
+    ne_finish(ne, N);
+    qr = ne_solve(ne, rcond, a);
+  }
+  if (qr)
+    qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
+      ptm_row_d(lu[base + n], lv[base + n], r);
+      L = ld_d(I + base + n);
+    }, a);
   store_coef<TC, LAYOUT>(coef, P, p, a);
 }
 
