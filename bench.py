@@ -60,6 +60,10 @@ CONFIGS = {
     "c8n200": ("rbf_perpixel", 400, 400, 200, 1, "rbf",
                "reference default pipeline at N=200 (SURVEY §6): per-pixel linear RBF of a 400x400 ROI x 200 lights "
                "on the 100x100 grid -> int32 tables"),
+    "c8n400": ("rbf_perpixel", 400, 400, 400, 1, "rbf",
+               "reference default pipeline above 256 lights (a 100 s capture: N = frames/8, analysis.py:120,152): "
+               "per-pixel linear RBF of a 400x400 ROI x 400 lights (blocked fp64 Cholesky) on the 100x100 grid -> "
+               "int32 tables"),
     "c9": ("frame", 2160, 3840, 1000, 1, "ptm",
            "interactive relight frame 3840x2160 (relighting_event): PTM-6 maps at one cursor (lu,lv) -> int32 -> "
            "clip -> V of the HSV ROI -> OpenCV HSV2BGR, one launch per event"),

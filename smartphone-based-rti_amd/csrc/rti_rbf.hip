@@ -10,7 +10,8 @@
 // pixel and solves its N×N system — fp64 Gauss-Jordan in registers up to N = 80, above that
 // (to N = 256; the systems reach cond ≈ 1e4–1e5 at N = 100–200) an fp32 Gauss-Jordan inverse of
 // the Householder-projected system held in registers as 8×8 blocks, plus fp64 iterative
-// refinement — and a second kernel streams the E evaluations in fp64.
+// refinement, above N = 256 a blocked fp64 Cholesky of the same system in global memory
+// (rbf_solve_chol) — and a second kernel streams the E evaluations in fp64.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -897,6 +898,338 @@ rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const
   }
 }
 
+// ---- Blocked fp64 Cholesky of the bordered system (N > 256; no cap) ------------------------------
+// The register-blocked inverses stop at N = 256 (an 8·32-row grid of 8×8 fp32 blocks is the whole
+// register file); the reference takes N = frames/8 lights (analysis.py:120,152), beyond 256 for any
+// capture over ≈ 68 s.  For those N the same bordered system (see rbf_solve_gji:
+// S = −(HAH)[:n, :n] symmetric positive definite, n = N − 1) is factored S = L Lᵀ in fp64 — SciPy's fp64
+// accuracy without refinement — by a right-looking blocked Cholesky whose matrix lives in a per-workgroup
+// slot of global memory ([ld][ld] doubles, lower triangle, L2/MALL-resident while the slot is hot):
+//   per panel of NB columns: the panel rows [k0, n) are staged in LDS, the NB×NB diagonal block is
+//   factored by wave 0 (wave-synchronous), the rows below are solved against it (a triangular solve per
+//   row, one thread per row), the panel is written back, and the trailing lower triangle is updated
+//   S[i][j] −= Σ_q L[i][q]·L[j][q] in 8×8 register tiles (4 FMAs per LDS read);
+// then L y = [c₁ | m] and Lᵀ z = y by blocked substitutions (diagonal blocks on wave 0, the off-diagonal
+// products over the threads), the bordered elimination gives y_n and w = H y.  One workgroup per CU strides
+// over the pixels (its slot is reused pixel after pixel).  A non-positive fp64 pivot (nodes closer than
+// fp64 can separate, or repeated ones) reports RTI_ERR_SINGULAR with NaN weights, where SciPy raises
+// LinAlgError for repeated nodes.  Cost ≈ n³/3 fp64 FMAs per pixel (SciPy's LU: 2n³/3).
+constexpr int RBF_CH_THREADS = 512;
+constexpr size_t RBF_CH_LDS = 160 * 1024 - 256;  // dynamic LDS per workgroup (the static part is < 256 B)
+
+// LDS of one workgroup: the panel [N][NB + 1] doubles (a bank shift per row), the two right-hand sides /
+// solutions [2][N] doubles and the nodes [2][N] floats.
+__host__ __device__ constexpr size_t chol_lds_bytes(int N, int NB) { return (size_t)N * (8 * NB + 8 + 16 + 8); }
+// widest panel whose LDS fits: 32 to N = 568, 16 to 1022, 8 to 1704, 4 to 2556 (0: too many lights)
+__host__ __device__ constexpr int chol_nb(int N) {
+  return chol_lds_bytes(N, 32) <= RBF_CH_LDS ? 32
+         : chol_lds_bytes(N, 16) <= RBF_CH_LDS ? 16
+         : chol_lds_bytes(N, 8) <= RBF_CH_LDS ? 8
+         : chol_lds_bytes(N, 4) <= RBF_CH_LDS ? 4 : 0;
+}
+constexpr int RBF_CH_MAX_N = 2556;
+static_assert(chol_nb(RBF_CH_MAX_N) == 4 && chol_nb(RBF_CH_MAX_N + 1) == 0, "RBF_CH_MAX_N");
+
+__host__ __device__ constexpr int chol_ld(int N) { return (N + 31) / 32 * 32; }
+// per-workgroup slot in global memory: M [ld][ld] (lower triangle) + the vectors g (= A u), c, m ([ld] each)
+__host__ __device__ constexpr int64_t chol_slot_doubles(int N) { return (int64_t)chol_ld(N) * chol_ld(N) + 3 * chol_ld(N); }
+
+// Phase timer for tools/probe/chol_probe.hip (compiled in only there): per workgroup, the steady-clock
+// ticks spent in each phase, summed over its pixels (a barrier closes every phase).
+#ifdef RTI_CHOL_PROFILE
+__device__ unsigned long long rti_chol_prof[1024][16];
+#define CH_MARK(k)                                   \
+  do {                                               \
+    __syncthreads();                                 \
+    if (t == 0) {                                    \
+      const long long now_ = wall_clock64();         \
+      prof_[k] += now_ - last_;                      \
+      last_ = now_;                                  \
+    }                                                \
+  } while (0)
+#else
+#define CH_MARK(k) \
+  do {             \
+  } while (0)
+#endif
+
+template <int NB, typename T>
+__global__ void __launch_bounds__(RBF_CH_THREADS)
+rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
+               double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status,
+               double* __restrict__ ws) {
+  static_assert(NB <= 32, "a wave solves both right-hand sides of a diagonal block (2·NB lanes)");
+  constexpr int TH = RBF_CH_THREADS, LDP = NB + 1;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* pan = smem;                                        // [N][LDP]
+  double* y1 = pan + (size_t)N * LDP;                        // c₁ -> L⁻¹c₁ -> S⁻¹c₁
+  double* y2 = y1 + N;                                       // m  -> L⁻¹m  -> S⁻¹m
+  float* xs = reinterpret_cast<float*>(y2 + N);
+  float* ys = xs + N;
+  __shared__ double red[TH / 64];
+  __shared__ int s_bad;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = N - 1, ld = chol_ld(N);
+  double* M = ws + (int64_t)blockIdx.x * chol_slot_doubles(N);
+  double* gv = M + (int64_t)ld * ld;  // g = A u
+  double* cv = gv + ld;               // c = H b
+  double* mv = cv + ld;               // m = (HAH)[:n, n], μ at n
+  const double e = 1.0 / sqrt((double)N), beta = 1.0 / (1.0 - e);  // H = I − β u uᵀ, u = e·1 − e_n
+  auto u = [&](int j) { return j < n ? e : (j == n ? e - 1.0 : 0.0); };
+  auto sum_all = [&](double v) {  // block-wide sum, every thread gets it
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    __syncthreads();  // the previous sum's readers are done with red
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < TH / 64; ++i) r += red[i];
+    return r;
+  };
+  auto dist = [&](int i, int j) { return dist64((double)xs[i], (double)ys[i], (double)xs[j], (double)ys[j]); };
+#ifdef RTI_CHOL_PROFILE
+  long long prof_[16] = {}, last_ = wall_clock64();
+#endif
+  // one diagonal block's two triangular solves on wave 0: lanes r and 32 + r hold row r's entries of the
+  // two right-hand sides; L[r][c] at Ld[r·LDP + c].  Forward: L z = s; backward: Lᵀ z = s.
+  const int r32 = lane & 31;
+  auto diag_solve = [&](const double* Ld, int kb, double* ya, double* yb, bool backward) {
+    double v = r32 < kb ? (lane < 32 ? ya[r32] : yb[r32]) : 0.0;
+    for (int i = 0; i < kb; ++i) {
+      const int c = backward ? kb - 1 - i : i;
+      if (r32 == c) v /= Ld[c * LDP + c];
+      const double zc = __shfl(v, (lane & 32) + c, 64);
+      if (backward ? r32 < c : (r32 > c && r32 < kb)) v = fma(backward ? -Ld[c * LDP + r32] : -Ld[r32 * LDP + c], zc, v);
+    }
+    if (r32 < kb) (lane < 32 ? ya : yb)[r32] = v;
+  };
+
+  for (int64_t p = blockIdx.x; p < P; p += gridDim.x) {
+    const int64_t base = p * N;
+    if (t == 0) s_bad = 0;
+    for (int j = t; j < N; j += TH) {
+      const float x = lu[base + j], y = lv[base + j];
+      xs[j] = x, ys[j] = y;
+      xyT[(int64_t)j * P + p] = make_float2(x, y);
+      y1[j] = ldd(I + base + j);  // b (y1 holds b until c is formed)
+    }
+    __syncthreads();
+    CH_MARK(0);
+    // A's lower triangle into M (one wave per row, coalesced) with its row sums, and the repeated-node
+    // check (SciPy: LinAlgError); each distance is evaluated once
+    bool dup = false;
+    for (int i = wave; i < N; i += TH / 64) {
+      double rs = 0.0;
+      for (int j = lane; j <= i; j += 64) {
+        const double d = dist(i, j);
+        M[(int64_t)i * ld + j] = d;
+        rs += d;
+        dup = dup || (j != i && d == 0.0);
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+      if (lane == 0) y2[i] = rs;
+    }
+    if (dup) s_bad = 1;
+    __syncthreads();
+    CH_MARK(1);
+    // g = A u = e·(row sums) − A[:, n]: add the upper part of each row sum (a column of the lower
+    // triangle, coalesced over i)
+    for (int i = t; i < N; i += TH) {
+      double rs = y2[i];
+      for (int j = i + 1; j < N; ++j) rs += M[(int64_t)j * ld + i];
+      gv[i] = fma(e, rs, -(i < n ? M[(int64_t)n * ld + i] : 0.0));
+    }
+    __syncthreads();
+    CH_MARK(2);
+    double ub = 0.0, ug = 0.0;
+    for (int i = t; i < N; i += TH) ub = fma(u(i), y1[i], ub), ug = fma(u(i), gv[i], ug);
+    const double utb = sum_all(ub), b2 = beta * beta * sum_all(ug);
+    // HAH from the stored distances (i >= j)
+    auto hah = [&](int i, int j, double d) { return d - beta * (u(i) * gv[j] + gv[i] * u(j)) + b2 * u(i) * u(j); };
+    for (int i = t; i < N; i += TH) {
+      const double ci = y1[i] - beta * u(i) * utb, mi = hah(n, i, i < n ? M[(int64_t)n * ld + i] : 0.0);
+      cv[i] = ci, mv[i] = mi, y1[i] = ci, y2[i] = mi;
+    }
+    __syncthreads();  // row n of M is read above; S overwrites rows [0, n) only, but keep the phases apart
+    // S = −(HAH)[:n, :n] in place, lower triangle, one wave per row
+    for (int i = wave; i < n; i += TH / 64)
+      for (int j = lane; j <= i; j += 64) {
+        double* mij = M + (int64_t)i * ld + j;
+        *mij = -hah(i, j, *mij);
+      }
+    __syncthreads();
+    CH_MARK(3);
+
+    // ---- blocked Cholesky S = L Lᵀ, with the forward substitutions L y = [c₁ | m] panel by panel --------
+    for (int k0 = 0; k0 < n && !s_bad; k0 += NB) {  // s_bad: block-uniform after each sync
+      const int kb = min(NB, n - k0), rows = n - k0;
+      for (int idx = t; idx < rows * NB; idx += TH) {  // stage the panel rows [k0, n), columns [k0, k0 + kb)
+        const int r = idx / NB, c = idx - r * NB;
+        pan[r * LDP + c] = (c < kb && c <= r) ? M[(int64_t)(k0 + r) * ld + k0 + c] : 0.0;
+      }
+      __syncthreads();
+      CH_MARK(4);
+      if (wave == 0) {  // the diagonal block in registers: lane r holds row r, pivots broadcast by readlane
+        double a[NB];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) a[c] = r32 < kb && lane < 32 ? pan[r32 * LDP + c] : 0.0;
+        bool bad = false;
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+          if (c < kb) {
+            const double d = readlane64(a[c], c);
+            bad = bad || !(d > 0.0);
+            const double sd = sqrt(d), inv = 1.0 / sd;
+            a[c] = r32 == c ? sd : a[c] * inv;  // column c of L (rows > c), the pivot on the diagonal
+#pragma unroll
+            for (int q = c + 1; q < NB; ++q)
+              if (q < kb) a[q] = fma(-a[c], readlane64(a[c], q), a[q]);  // L[r][q] −= L[r][c]·L[q][c]
+          }
+        }
+        if (lane < 32 && r32 < kb) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c)
+            if (c <= r32) pan[r32 * LDP + c] = a[c];
+        }
+        if (bad && lane == 0) s_bad = 1;
+      }
+      __syncthreads();
+      CH_MARK(5);
+      if (s_bad) break;  // a non-positive pivot
+      // rows below the block: x·L_Dᵀ = panel row  ->  forward substitution against the diagonal block;
+      // wave 0 meanwhile solves the block's part of L y = [c₁ | m]
+      if (wave == 0) diag_solve(pan, kb, y1 + k0, y2 + k0, false);
+      for (int r = kb + t; r < rows; r += TH) {
+        double x[NB];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+          if (c < kb) {
+            double s = pan[r * LDP + c];
+#pragma unroll
+            for (int q = 0; q < c; ++q) s = fma(-x[q], pan[c * LDP + q], s);
+            x[c] = s / pan[c * LDP + c];
+          } else {
+            x[c] = 0.0;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < NB; ++c)
+          if (c < kb) pan[r * LDP + c] = x[c];
+      }
+      __syncthreads();
+      CH_MARK(6);
+      for (int idx = t; idx < rows * NB; idx += TH) {  // write L's panel back (for the backward substitution)
+        const int r = idx / NB, c = idx - r * NB;
+        if (c < kb && c <= r) M[(int64_t)(k0 + r) * ld + k0 + c] = pan[r * LDP + c];
+      }
+      for (int r = kb + t; r < rows; r += TH) {  // y[i] −= L[i][k0:k0+kb]·y_block (LDS)
+        double s1 = y1[k0 + r], s2 = y2[k0 + r];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          if (q < kb) {
+            const double l = pan[r * LDP + q];
+            s1 = fma(-l, y1[k0 + q], s1);
+            s2 = fma(-l, y2[k0 + q], s2);
+          }
+        }
+        y1[k0 + r] = s1, y2[k0 + r] = s2;
+      }
+      CH_MARK(7);
+      // trailing update of the lower triangle of rows/columns [k0 + kb, n): a wave per 64×32 tile, lane
+      // (x, y) = (lane & 7, lane >> 3) owns rows y + 8a (a < 8) and columns x + 8b (b < 4) — each LDS read
+      // touches 8 distinct panel rows (distinct banks with the NB + 1 pitch), broadcast over 8 lanes;
+      // 12 reads per 32 fp64 FMAs
+      const int m = rows - kb, T64 = (m + 63) / 64, nst = T64 * (T64 + 1);  // row tile I: 2I + 2 column tiles
+      const int lx = lane & 7, ly = lane >> 3;
+      for (int st = wave; st < nst; st += TH / 64) {
+        int I64 = 0;
+        while ((I64 + 1) * (I64 + 2) <= st) ++I64;  // st -> (I64, J32), J32 <= 2·I64 + 1 (wave-uniform)
+        const int J32 = st - I64 * (I64 + 1);
+        const int ri = kb + 64 * I64 + ly, rj = kb + 32 * J32 + lx;
+        if (32 * J32 >= m) continue;  // past the trailing block (the last row tile's right half)
+        double acc[8][4];
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+        for (int q = 0; q < kb; ++q) {
+          double li[8], lj[4];
+#pragma unroll
+          for (int a = 0; a < 8; ++a) li[a] = pan[min(ri + 8 * a, rows - 1) * LDP + q];  // rows past n: clamped
+#pragma unroll
+          for (int b = 0; b < 4; ++b) lj[b] = pan[min(rj + 8 * b, rows - 1) * LDP + q];  // reads, masked below
+#pragma unroll
+          for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) acc[a][b] = fma(li[a], lj[b], acc[a][b]);
+        }
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+          if (ri + 8 * a >= rows) continue;
+          double* row = M + (int64_t)(k0 + ri + 8 * a) * ld + k0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            if (rj + 8 * b < rows && rj + 8 * b <= ri + 8 * a) row[rj + 8 * b] -= acc[a][b];
+        }
+      }
+      __syncthreads();
+      CH_MARK(8);
+    }
+
+    if (s_bad) {
+      if (t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
+      for (int j = t; j < N; j += TH) wT[(int64_t)j * P + p] = __builtin_nan("");
+      __syncthreads();
+      continue;
+    }
+    // ---- Lᵀ z = y (backward), blocked by NB: diagonal blocks staged in LDS (the panel is free) --------
+    for (int k0 = (n - 1) / NB * NB; k0 >= 0; k0 -= NB) {
+      const int kb = min(NB, n - k0);
+      for (int idx = t; idx < kb * NB; idx += TH) {
+        const int r = idx / NB, c = idx - r * NB;
+        if (c <= r) pan[r * LDP + c] = M[(int64_t)(k0 + r) * ld + k0 + c];
+      }
+      __syncthreads();
+      if (wave == 0) diag_solve(pan, kb, y1 + k0, y2 + k0, true);
+      __syncthreads();
+      for (int i = t; i < k0; i += TH) {  // y[i] −= Σ_q L[k0+q][i]·z[k0+q]: rows of L, coalesced over i
+        double s1 = y1[i], s2 = y2[i];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          if (q < kb) {
+            const double l = M[(int64_t)(k0 + q) * ld + i];
+            s1 = fma(-l, y1[k0 + q], s1);
+            s2 = fma(-l, y2[k0 + q], s2);
+          }
+        }
+        y1[i] = s1, y2[i] = s2;
+      }
+      __syncthreads();
+    }
+    CH_MARK(9);
+    // bordered elimination: y_n = (c_n + mᵀz1)/(μ + mᵀz2), y₁ = −z1 + z2·y_n, w = H y
+    double a1 = 0.0, a2 = 0.0;
+    for (int i = t; i < n; i += TH) a1 = fma(mv[i], y1[i], a1), a2 = fma(mv[i], y2[i], a2);
+    const double mz1 = sum_all(a1), mz2 = sum_all(a2);
+    const double yn = (cv[n] + mz1) / (mv[n] + mz2);
+    double uy = 0.0;
+    for (int i = t; i < N; i += TH) uy = fma(u(i), i < n ? -y1[i] + y2[i] * yn : yn, uy);
+    const double uty = sum_all(uy);
+    for (int i = t; i < N; i += TH) {
+      const double yi = i < n ? -y1[i] + y2[i] * yn : yn;
+      wT[(int64_t)i * P + p] = yi - beta * u(i) * uty;
+    }
+    __syncthreads();  // the slot, the vectors, xs/ys and the panel are reused by the next pixel
+    CH_MARK(10);
+  }
+#ifdef RTI_CHOL_PROFILE
+  if (t == 0 && blockIdx.x < 1024)
+    for (int k = 0; k < 16; ++k) rti_chol_prof[blockIdx.x][k] = prof_[k];
+#endif
+}
+
 // fp64 register Gauss-Jordan up to here, rbf_solve_gji above (solve of a 400×400 ROI, MI355X:
 // N = 64: 6.3 vs 13.2 ms, N = 96: 27.9 vs 18.1 ms; tools/time_rbf_solve.py)
 constexpr int RBF_GJ_MAX_N = 80;
@@ -922,9 +1255,25 @@ bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); 
 // redo / fb_ws: the flag per pixel (zeroed) and the fp64 fallback's workspace, when uses_gji(N)
 template <typename T>
 void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
-                  int* status, int* redo, double* fb_ws, hipStream_t s) {
+                  int* status, int* redo, double* fb_ws, int64_t chol_grid, hipStream_t s) {
   const T* In = static_cast<const T*>(I);
   const dim3 g((unsigned)P);
+  if (N > RBF_MAX_N) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
+    const unsigned cg = (unsigned)(P < chol_grid ? P : chol_grid);
+    auto go = [&](auto kern) {
+      const size_t lds = chol_lds_bytes(N, chol_nb(N));
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      hipLaunchKernelGGL(kern, dim3(cg), dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
+    };
+    switch (chol_nb(N)) {
+      case 32: go(rbf_solve_chol<32, T>); break;
+      case 16: go(rbf_solve_chol<16, T>); break;
+      case 8: go(rbf_solve_chol<8, T>); break;
+      default: go(rbf_solve_chol<4, T>); break;
+    }
+    return;
+  }
   if (uses_gji(N)) {
     if (N <= 128)
       hipLaunchKernelGGL((rbf_solve_gji<16, T>), g, dim3(256), 0, s, lu, lv, In, N, P, wT, xyT, status, redo,
@@ -981,7 +1330,8 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
                                 rti_stream_t stream) {
   if (!lu || !lv || !I || !luv || !out || !status) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: null pointer");
   if (N <= 0 || P <= 0 || E <= 0) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: N, P, E must be positive");
-  if (N > RBF_MAX_N) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: N=%d > %d lights", N, RBF_MAX_N);
+  if (N > RBF_CH_MAX_N)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: N=%d > %d lights", N, RBF_CH_MAX_N);
   if (P > 0x7fffffff) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: P too large for one launch");
   if (in_dtype != RTI_F32 && in_dtype != RTI_U8 && in_dtype != RTI_I32)
     return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: input dtype %d", in_dtype);
@@ -995,8 +1345,11 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
   // workspace: per-pixel weights and nodes, node-major ([N][P]) for the coalesced evaluation
   void* ws = nullptr;
   // + for the block solvers: a redo flag per pixel and the fp64 fallback's per-workgroup matrices
-  const bool fb = uses_gji(N);
-  const size_t fb_ws_bytes = fb ? (size_t)RBF_FB_GRID * N * (N + 1) * sizeof(double) : 0;
+  const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
+  // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
+  const int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
+  const size_t fb_ws_bytes = fb ? (size_t)RBF_FB_GRID * N * (N + 1) * sizeof(double)
+                                : (chol ? (size_t)chol_grid * chol_slot_doubles(N) * sizeof(double) : 0);
   const size_t flag_bytes = fb ? ((size_t)P * sizeof(int) + 255) / 256 * 256 : 0;
   const size_t bytes = (size_t)N * P * (sizeof(double) + sizeof(float2)) + fb_ws_bytes + flag_bytes;
   if (hipMallocAsync(&ws, bytes, s) != hipSuccess)
@@ -1010,9 +1363,9 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
     return fail(RTI_ERR_HIP, "rti_rbf_perpixel: clearing the redo flags failed");
   }
   switch (in_dtype) {
-    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, s); break;
-    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, s); break;
-    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, s); break;
+    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, s); break;
+    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, s); break;
+    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, s); break;
   }
   switch (out_dtype) {
     case RTI_F64: launch_eval<double>(out_layout, wT, xyT, N, P, luv, E, out, s); break;

@@ -86,6 +86,33 @@ def test_operator_ragged_vs_oracle(cuda, hw, n, E, precision):
     assert ok, err
 
 
+@pytest.mark.parametrize("n", [257, 300, 512, 513, 700, 1100])
+def test_operator_many_lights(cuda, n):
+    """Above 256 lights AUTO applies the fp32 operator (v_mfma_f32_16x16x4_f32): the tile is staged once to
+    N = 512, beyond that the light chunks are restaged per row tile.  Fused PTM fit + evaluation and the
+    shared-light RBF interpolation (analysis.py:249-260, the reference has no light cap) against the oracle."""
+    h, w, E = 9, 37, 300
+    lu, lv = o.synth_dirs(n, n)
+    I = o.synth_intensities(h, w, lu, lv, seed=n)
+    rng = np.random.default_rng(n)
+    qu, qv = rng.uniform(-1, 1, E), rng.uniform(-1, 1, E)
+    out = rti.apply_operator(rti.basis_operator(lu, lv, qu, qv, "ptm"), torch.as_tensor(I, device=cuda))
+    ref = o.relight(o.fit_shared(I, o.pinv_shared("ptm", lu, lv)), "ptm", qu, qv).reshape(E, h, w)
+    err, ok = relight_close(out.cpu().numpy(), ref, rtol=1e-5)
+    assert ok, err
+    sub = np.moveaxis(np.round(I[:, :2, :2]).astype(np.int32), 0, -1)  # 4 pixels [y][x][n], compat's layout
+    lx = np.broadcast_to(lu, (2, 2, n)).copy()
+    ly = np.broadcast_to(lv, (2, 2, n)).copy()
+    gu, gv = grid_q()
+    ref = np.stack([o.rbf_linear(lu, lv, sub[y, x], gu, gv) for y in range(2) for x in range(2)])
+    got = compat.interpolate_intensities((lx, ly, sub)).reshape(4, -1)
+    # the fp32 operator's bound: |err| <= 1e-5 · Σ_n |M_en| |I_n| (M = Φ A⁻¹ grows with cond(A))
+    op = rti.rbf_operator(lu, lv, gu, gv)
+    bound = 1e-5 * (np.abs(sub.reshape(4, n)) @ np.abs(op))
+    err = np.abs(got - ref)
+    assert (err <= np.maximum(bound, 1e-9)).all(), float((err / np.maximum(bound, 1e-9)).max())
+
+
 @pytest.mark.parametrize("precision", ["split16", "fp32"])
 def test_operator_channels_and_int_outputs(cuda, precision):
     lu, lv = o.synth_dirs(30, 2)
@@ -165,13 +192,15 @@ def test_compat_default_interpolation_perpixel(cuda):
         compat.interpolate_intensities((d["singular_lx"], d["singular_ly"], d["I"][:1, :1]))
 
 
-@pytest.mark.parametrize("n", [2, 6, 37, 64, 65, 80, 81, 100, 127, 128, 129, 160, 200, 248, 249, 255, 256])
+@pytest.mark.parametrize("n", [2, 6, 37, 64, 65, 80, 81, 100, 127, 128, 129, 160, 200, 248, 249, 255, 256,
+                               257, 300, 400, 512, 568, 569, 1100, 1800])
 def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     """Every solver of rti_rbf_perpixel: fp64 register Gauss-Jordan (N <= 80) and the register-blocked
     fp32 Gauss-Jordan inverse + fp64 refinement on the full 16x16 block grid (N <= 128), the
     lower-triangle block grid (N <= 248) and the full 32x32 grid (N <= 256) (SURVEY §6 timed the
-    reference at N = 200), each with the reference's per-pixel geometry, against SciPy's fp64 solve
-    restated in the oracle."""
+    reference at N = 200), and above 256 lights the blocked fp64 Cholesky (panels of 32 lights to N = 568,
+    16 to 1022, 8 to 1704, 4 to 2556; the reference takes N = frames/8, analysis.py:120,152), each with
+    the reference's per-pixel geometry, against SciPy's fp64 solve restated in the oracle."""
     ys, xs = np.mgrid[0:3, 0:5]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
@@ -184,10 +213,11 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     assert ok, err
 
 
-@pytest.mark.parametrize("n", [81, 128, 129, 200, 256])
+@pytest.mark.parametrize("n", [81, 128, 129, 200, 256, 257, 400, 600])
 def test_rbf_perpixel_large_n_repeated_node_raises(cuda, n):
-    """A repeated light direction makes A exactly singular: SciPy raises LinAlgError; so does the
-    block Gauss-Jordan solver; N > 256 is refused (RTI_ERR_UNSUPPORTED)."""
+    """A repeated light direction makes A exactly singular: SciPy raises LinAlgError; so do the
+    block Gauss-Jordan and the blocked Cholesky solvers; N above the Cholesky panels' LDS limit
+    (2556 lights: a 10-minute capture at 30 fps) is refused (RTI_ERR_UNSUPPORTED)."""
     ys, xs = np.mgrid[0:2, 0:2]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
@@ -198,11 +228,11 @@ def test_rbf_perpixel_large_n_repeated_node_raises(cuda, n):
     with pytest.raises(np.linalg.LinAlgError):
         rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv)
     with pytest.raises(NotImplementedError):
-        rti.interpolate_rbf_perpixel(torch.zeros((1, 257), dtype=torch.int32, device=cuda),
-                                     np.zeros((1, 257), np.float32), np.zeros((1, 257), np.float32), qu, qv)
+        rti.interpolate_rbf_perpixel(torch.zeros((1, 2557), dtype=torch.int32, device=cuda),
+                                     np.zeros((1, 2557), np.float32), np.zeros((1, 2557), np.float32), qu, qv)
 
 
-@pytest.mark.parametrize("n", [100, 200, 256])
+@pytest.mark.parametrize("n", [100, 200, 256, 300])
 @pytest.mark.parametrize("d", [1e-5, 1e-6, 1e-7])
 def test_rbf_perpixel_near_repeated_nodes_fp64_fallback(cuda, n, d):
     """Nearly repeated light directions (cond(A) ~ 1e7 .. 2e9): SciPy's fp64 LU still solves them, the
