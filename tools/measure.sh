@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-2 measurement pass on one MI355X box: every bench config under
+# Measurement pass (TAG=rNN) on one MI355X box: every bench config under
 # rocprofv3 --kernel-trace --stats (bench line + kernel stats of the same command),
 # the L3-resident relight for comparison, and PMC traffic passes.
-# Output under gpurun_out/r02/.
+# Output under gpurun_out/$TAG/.
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/r02
+out=gpurun_out/${TAG:-r03}
 mkdir -p $out
 run() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2
@@ -17,9 +17,9 @@ run() {  # name seconds cmd...
   return 0
 }
 for c in ${CONFIGS:-c3 c2 c4 c10 c5 c9 c6 c7 c8 c8n200}; do
-  budget=8; [ $c = c3 ] && budget=16; extra=""; [ $c = c8n200 ] && extra="--no-cpu"
-  run bench_$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_$c -o run -- \
-      python3 bench.py --config $c --cpu-budget $budget $extra
+  budget=8; [ $c = c3 ] && budget=16; extra=""; case $c in c8n200|c8n400) extra="--no-cpu";; esac
+  run bench_$c$SUFFIX 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_$c$SUFFIX -o run -- \
+      python3 bench.py --config $c --cpu-budget $budget $extra $BENCH_ARGS
 done
 if [ -z "$SKIP_EXTRA" ]; then
   run bench_c5_hot 200 python3 bench.py --config c5 --map-sets 1 --no-cpu
