@@ -1216,9 +1216,10 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
       int st;
       switch (in_dtype) {
         case RTI_F32: {
-          // launch generations for the 4096-pixel tile_w kernels (AUTO, or explicit 8 / 4 waves at rc >= 12:
-          // one workgroup per CU); the other tile forms stay one launch
-          const bool w4096 = tile_auto || ((waves == 8 || waves == 4) && rc >= 12);
+          // launch generations for the 4096-pixel tile_w kernels (AUTO, or explicit 8 waves at depth 1 /
+          // 4 waves, rc >= 12: one workgroup per CU; launch_tile_w runs a 2048-pixel tile at depth 2+);
+          // the other tile forms stay one launch
+          const bool w4096 = tile_auto || (rc >= 12 && (waves == 4 || (waves == 8 && depth == 1)));
           if (w4096 && !(kernel & RTI_KERNEL_ONE_LAUNCH)) gens = tile_generations(a, 4096);
           st = launch_generations(a, es, gens, [&](const FitArgs& b) {
             return tile_auto ? launch_tile<float>(b, 15, 1, 1, 8)

@@ -811,8 +811,8 @@ rbf_eval(const double* __restrict__ wT, const float2* __restrict__ xyT, int N, i
 // row), the system left diagonal, w at node k = b_p / a_pk of step k's pivot row p.  A fixed grid of
 // workgroups strides over the pixels 256 at a time (one flag load per thread, the flagged pixels
 // listed in LDS), so a launch without flagged pixels costs one coalesced pass over the flags.
+// The grid is one workgroup per CU (device_cus(), 256 on MI355X); each holds one N·(N+1) fp64 slot.
 constexpr int RBF_FB_THREADS = 256;
-constexpr int RBF_FB_GRID = 256;
 
 template <typename T>
 __global__ void __launch_bounds__(RBF_FB_THREADS)
@@ -1255,7 +1255,7 @@ bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); 
 // redo / fb_ws: the flag per pixel (zeroed) and the fp64 fallback's workspace, when uses_gji(N)
 template <typename T>
 void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
-                  int* status, int* redo, double* fb_ws, int64_t chol_grid, hipStream_t s) {
+                  int* status, int* redo, double* fb_ws, int64_t chol_grid, int64_t fb_grid, hipStream_t s) {
   const T* In = static_cast<const T*>(I);
   const dim3 g((unsigned)P);
   if (N > RBF_MAX_N) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
@@ -1284,7 +1284,7 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
     else
       hipLaunchKernelGGL((rbf_solve_gji<32, T>), g, dim3(1024), 0, s, lu, lv, In, N, P, wT, xyT, status, redo,
                          gji_refine());
-    const unsigned fg = (unsigned)(P < RBF_FB_GRID ? P : RBF_FB_GRID);
+    const unsigned fg = (unsigned)(P < fb_grid ? P : fb_grid);
     hipLaunchKernelGGL((rbf_solve_fp64<T>), dim3(fg), dim3(RBF_FB_THREADS), 0, s, lu, lv, In, N, P, redo, fb_ws, wT,
                        status);
     return;
@@ -1348,7 +1348,8 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
   const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
   const int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
-  const size_t fb_ws_bytes = fb ? (size_t)RBF_FB_GRID * N * (N + 1) * sizeof(double)
+  const int64_t fb_grid = fb ? (P < device_cus() ? P : device_cus()) : 0;
+  const size_t fb_ws_bytes = fb ? (size_t)fb_grid * N * (N + 1) * sizeof(double)
                                 : (chol ? (size_t)chol_grid * chol_slot_doubles(N) * sizeof(double) : 0);
   const size_t flag_bytes = fb ? ((size_t)P * sizeof(int) + 255) / 256 * 256 : 0;
   const size_t bytes = (size_t)N * P * (sizeof(double) + sizeof(float2)) + fb_ws_bytes + flag_bytes;
@@ -1363,9 +1364,9 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
     return fail(RTI_ERR_HIP, "rti_rbf_perpixel: clearing the redo flags failed");
   }
   switch (in_dtype) {
-    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, s); break;
-    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, s); break;
-    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, s); break;
+    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, s); break;
+    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, s); break;
+    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, s); break;
   }
   switch (out_dtype) {
     case RTI_F64: launch_eval<double>(out_layout, wT, xyT, N, P, luv, E, out, s); break;
