@@ -69,6 +69,7 @@ extern "C" {
 #define RTI_KERNEL_NT_STORE    0x400  /* non-temporal coefficient stores */
 #define RTI_KERNEL_STAGE       0x800  /* pixel-major output transposed through LDS (1 KiB stores) */
 #define RTI_KERNEL_ROTATE      0x10000000  /* AUTO PTM-6 fp32: each wave starts its light sweep at its own plane (measurement variant) */
+#define RTI_KERNEL_ROUNDS      0x40000000  /* AUTO PTM-6 fp32/int32: launch generations as rounds of one launch (rti_fit.hip) */
 #define RTI_KERNEL_ONE_LAUNCH  0x20000000  /* AUTO: one launch, no launch generations (measurement variant; rti_fit.hip) */
 /* VALU chunks per lane (bits 12-15; 0 = AUTO): a wave reads chunks*1 KiB contiguous per plane */
 #define RTI_KERNEL_CHUNKS_SHIFT 12

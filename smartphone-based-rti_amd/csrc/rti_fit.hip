@@ -286,6 +286,41 @@ fit_shared_valu(const float* __restrict__ pinv, int N, const T* __restrict__ I, 
     fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, true>(pinv, N, Ic, P, pe, lstride, dst, pbase, wave_base, lds_w, lds_dyn);
 }
 
+// Launch generations as rounds of ONE launch (RTI_KERNEL_ROUNDS): the grid is one generation's waves
+// (`per` waves of NC·64·VEC pixels), and wave gw handles, in round r = (channel, part), the pixels
+// [pb + part·span + gw·W, …) of that channel.  Every wave starts every round together with the others
+// (equal work per round), as the separate launches of launch_generations do, but a round's coefficient
+// stores drain while the next round's loads are already in flight, and no launch boundary (tail, ramp)
+// separates the rounds.
+template <int K, int VEC, int NC, typename T, int LAYOUT, int MODE>
+__global__ void __launch_bounds__(256)
+fit_shared_valu_rounds(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t span,
+                       int parts, int rounds, int64_t lstride, int64_t cstride, float* __restrict__ coef,
+                       int64_t ocstride) {
+  constexpr bool LDSW = (MODE & VM_LDS) != 0;
+  static_assert(!LDSW, "rounds: SGPR weights only");
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  constexpr int64_t WPX = 64 * VEC * NC;  // pixels per wave and round
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+  for (int r = 0; r < rounds; ++r) {
+    const int c = r / parts, part = r - c * parts;
+    const int64_t rb = (int64_t)part * span, re = rb + span < P ? rb + span : P;
+    const int64_t wave_base = rb + gw * WPX;
+    if (wave_base >= re) continue;  // wave-uniform
+    const int64_t pbase = wave_base + (int64_t)lane * VEC;
+    const T* __restrict__ Ic = I + (int64_t)c * cstride;
+    float* __restrict__ dst = coef + (int64_t)c * ocstride;
+    if (wave_base + WPX <= re) {  // wave-uniform
+      fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, false>(pinv, N, Ic, P, re, lstride, dst, pbase, wave_base, lds_dyn,
+                                                         lds_dyn);
+    } else if (pbase < re) {
+      fit_valu_body<K, VEC, NC, T, LAYOUT, MODE, true>(pinv, N, Ic, P, re, lstride, dst, pbase, wave_base, lds_dyn,
+                                                        lds_dyn);
+    }
+  }
+}
+
 // ---- MFMA kernel (k <= 16) ------------------------------------------------------------
 // Block = 4 waves; wave w owns the 64 pixels [p0, p0+64) with
 // p0 = (4·blockIdx.x + w)·64.  Lane l: q = l & 15 (MFMA column), r = l >> 4
@@ -610,6 +645,131 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
   }
 }
 
+// Tile STREAM form of the AHEAD = 0 kernel (RTI_KERNEL_ROUNDS): one workgroup per CU that streams
+// the tiles u = blockIdx.x, blockIdx.x + G, ... of the flattened (channel, tile) space (G = gridDim.x)
+// as ONE pipeline of ntiles·T steps, so only its first step waits for HBM cold, every workgroup sweeps
+// the planes in step with the others (the chip reads one contiguous G-tile slab of a plane at a time),
+// and a finished tile's coefficient stores drain while the next tile's loads are in flight, with no
+// launch boundary in between (the separate launches of the launch generations end in a write burst
+// and start with a cold ramp).  Every vector-memory operation of the loop is unconditional (lights
+// past N and pixels past P re-read valid addresses: the values are zeroed by selects, or never
+// stored), so the compiler's counted vmcnt waits stay exact; a finished tile's stores are issued at
+// the start of the next tile's first step, before that step's loads.
+template <int RC, int W, typename T, int LAYOUT, bool NT>
+__global__ void __launch_bounds__(64 * W)
+fit_shared_tile_s(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P, int64_t tpc,
+                  int64_t ntot, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  constexpr int R = 256 * RC, S = W, G = R / (64 * W);
+  static_assert(G >= 1 && R % (64 * W) == 0, "tile must split into 64-pixel groups per wave");
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  const int T_ = (N + S - 1) / S;
+  float* __restrict__ lds_pinv = lds_dyn;            // [T_·S][16]
+  float* __restrict__ tile = lds_dyn + T_ * S * 16;  // [S][R]
+  for (int idx = threadIdx.x; idx < T_ * S * 16; idx += 64 * W) {
+    const int n = idx >> 4, i = idx & 15;
+    lds_pinv[idx] = (i < k && n < N) ? pinv[i * N + n] : 0.f;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t Gw = gridDim.x;
+  const int ntiles = (int)((ntot - blockIdx.x + Gw - 1) / Gw);
+  const int steps = ntiles * T_;
+  auto tile_of = [&](int j, int& c, int64_t& t0) {
+    const int64_t u = blockIdx.x + (int64_t)j * Gw;
+    c = (int)(u / tpc);
+    t0 = (u - (int64_t)c * tpc) * R;
+  };
+  auto load = [&](int s, floatx4 (&st)[RC]) {
+    const int j = s / T_, t = s - j * T_;
+    int c;
+    int64_t t0;
+    tile_of(j, c, t0);
+    const int n = t * S + wave;
+    const bool nok = n < N;
+    const T* __restrict__ src = I + (int64_t)c * cstride + (int64_t)(nok ? n : N - 1) * lstride;
+#pragma unroll
+    for (int cc = 0; cc < RC; ++cc) {
+      int64_t px = t0 + 256 * cc + 4 * lane;
+      px = px < P ? px : P - 4;  // never stored
+      float x[4];
+      load_px<T, 4, NT>(src + px, x);
+      st[cc] = nok ? floatx4{x[0], x[1], x[2], x[3]} : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto park = [&](const floatx4 (&st)[RC]) {
+    float* __restrict__ tb = tile + wave * R;
+#pragma unroll
+    for (int cc = 0; cc < RC; ++cc) *reinterpret_cast<floatx4*>(tb + 256 * cc + 4 * lane) = st[cc];
+  };
+  const int q = lane & 15, r = lane >> 4;
+  const int pw = wave * 64 * G;
+  floatx4 acc[G][4];
+  auto zero = [&]() {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[g][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto compute = [&](int t) {
+#pragma unroll
+    for (int s = 0; s < S / 4; ++s) {
+      const float a = lds_pinv[(t * S + 4 * s + r) * 16 + q];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const floatx4 x = *reinterpret_cast<const floatx4*>(tile + (4 * s + r) * R + pw + 64 * g + 4 * q);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[g][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[c], acc[g][c], 0, 0, 0);
+      }
+    }
+  };
+  // acc[g][c][rr] = coefficient 4r + rr of pixel t0 + pw + 64g + 4q + c
+  auto finish = [&](int j) {
+    int c;
+    int64_t t0;
+    tile_of(j, c, t0);
+    float* __restrict__ dst = coef + (int64_t)c * ocstride;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t px = t0 + pw + 64 * g + 4 * q;
+      if (px >= P) continue;
+      if constexpr (LAYOUT == RTI_COEF_PLANAR) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int i = 4 * r + rr;
+          if (i < k)
+            *reinterpret_cast<floatx4*>(dst + (int64_t)i * P + px) =
+                floatx4{acc[g][0][rr], acc[g][1][rr], acc[g][2][rr], acc[g][3][rr]};
+        }
+      } else if (k == 16) {
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) *reinterpret_cast<floatx4*>(dst + (px + c4) * 16 + 4 * r) = acc[g][c4];
+      } else {
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            if (4 * r + rr < k) dst[(px + c4) * k + 4 * r + rr] = acc[g][c4][rr];
+      }
+    }
+    zero();
+  };
+  if (ntiles <= 0) return;  // workgroup-uniform
+  zero();
+  floatx4 sa[RC];
+  load(0, sa);
+  park(sa);
+  __syncthreads();
+  for (int s = 0; s < steps; ++s) {
+    const int j = s / T_, t = s - j * T_;
+    if (t == 0 && j > 0) finish(j - 1);  // the previous tile's stores, before this step's loads
+    load(s + 1 < steps ? s + 1 : s, sa);
+    compute(t);
+    __syncthreads();
+    park(sa);
+    __syncthreads();
+  }
+  finish(ntiles - 1);
+}
+
 // DMA form (fp32 stacks): the tile planes go HBM -> LDS by global_load_lds_dwordx4 (no VGPR
 // hop, 1 KiB per wave instruction) into a ring of NB tiles, NB - 1 steps in flight.  A step
 // waits for its own wave's DMAs with a counted vmcnt and one raw s_barrier publishes it to the
@@ -748,6 +908,10 @@ struct FitArgs {
   int nc;    // VALU chunks per lane (1 = one VEC-pixel group per lane)
   hipStream_t stream;
   int64_t pb = 0, pe = 0;  // this launch's pixel range [pb, pe) (pe 0 = P): VALU and 8-wave tile kernels
+  // VALU generations as rounds of one launch (fit_shared_valu_rounds): parts per channel (0 = off), the
+  // pixels per part and the waves of one round
+  int rparts = 0;
+  int64_t rspan = 0, rwaves = 0;
 };
 
 template <int K, int VEC, int NC, typename T, int LAYOUT, int MODE>
@@ -759,6 +923,17 @@ void launch_valu_t(const FitArgs& a) {
   size_t lds = (MODE & VM_LDS) ? (((size_t)a.N * KP + 3) & ~(size_t)3) * sizeof(float) : 0;
   if constexpr ((MODE & VM_STAGE) && LAYOUT == RTI_COEF_PIXEL_MAJOR && stage_ok<K, VEC>())
     lds += (size_t)4 * 64 * 4 * K * sizeof(float);  // 4 waves x 64 lanes x 4 pixels x K
+  // the forms AUTO's generations use (valu_generations: non-temporal loads, 4-pixel lanes, nc > 1)
+  if constexpr ((MODE & VM_NT) && !(MODE & (VM_LDS | VM_ROT | VM_NTS)) && NC > 1 && VEC == 4 && K == 6 &&
+                !std::is_same<T, uint8_t>::value) {
+    if (a.rparts > 0) {
+      const dim3 rgrid((unsigned)((a.rwaves + 3) / 4));
+      hipLaunchKernelGGL((fit_shared_valu_rounds<K, VEC, NC, T, LAYOUT, MODE>), rgrid, dim3(256), lds, a.stream,
+                         a.pinv, a.N, static_cast<const T*>(a.I), a.P, a.rspan, a.rparts, a.rparts * a.C, a.lstride,
+                         a.cstride, a.coef, a.ocstride);
+      return;
+    }
+  }
   hipLaunchKernelGGL((fit_shared_valu<K, VEC, NC, T, LAYOUT, MODE>), grid, dim3(256), lds, a.stream, a.pinv, a.N,
                      static_cast<const T*>(a.I), a.P, a.pb, pe, a.lstride, a.cstride, a.coef, a.ocstride);
 }
@@ -930,6 +1105,32 @@ int launch_tile_w(const FitArgs& a, int rc, int depth) {
   if (depth == 1) return rc >= 12 ? launch_tile_w_l<16, 0>(a) : launch_tile_w_l<8, 0>(a);  // CHUNKS(15) = 16
   if (rc >= 8) return depth >= 3 ? launch_tile_w_l<8, 2>(a) : launch_tile_w_l<8, 1>(a);
   return depth >= 3 ? launch_tile_w_l<4, 2>(a) : launch_tile_w_l<4, 1>(a);
+}
+
+// tile stream (fit_shared_tile_s): one workgroup per CU over the flattened (channel, tile) space
+template <int RC, int W, int LAYOUT, bool NT>
+int launch_tile_s_t(const FitArgs& a) {
+  constexpr int R = 256 * RC, S = W;
+  const int T_ = (a.N + S - 1) / S;
+  const size_t lds = ((size_t)T_ * S * 16 + (size_t)S * R) * sizeof(float);
+  if (lds > 160 * 1024)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
+  auto kern = fit_shared_tile_s<RC, W, float, LAYOUT, NT>;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
+  const int64_t tpc = (a.P + R - 1) / R, ntot = tpc * a.C, cus = device_cus();
+  const dim3 grid((unsigned)(ntot < cus ? ntot : cus));
+  hipLaunchKernelGGL(kern, grid, dim3(64 * W), lds, a.stream, a.pinv, a.k, a.N, static_cast<const float*>(a.I), a.P,
+                     tpc, ntot, a.lstride, a.cstride, a.coef, a.ocstride);
+  return RTI_OK;
+}
+
+int launch_tile_s(const FitArgs& a) {
+  if (a.layout == RTI_COEF_PLANAR)
+    return a.nt ? launch_tile_s_t<16, 8, RTI_COEF_PLANAR, true>(a) : launch_tile_s_t<16, 8, RTI_COEF_PLANAR, false>(a);
+  return a.nt ? launch_tile_s_t<16, 8, RTI_COEF_PIXEL_MAJOR, true>(a)
+              : launch_tile_s_t<16, 8, RTI_COEF_PIXEL_MAJOR, false>(a);
 }
 
 // 4-wave form of the same kernel at one wave per SIMD: a 4096-pixel tile (16 KiB per wave and
@@ -1186,6 +1387,13 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
       gnc = valu_generations(a, es, gens);
     if (gnc) {
       a.nc = gnc;
+      if ((kernel & RTI_KERNEL_ROUNDS) && gens.split) {  // the generations as rounds of one launch
+        const int64_t units = (P + gens.unit - 1) / gens.unit, per = (units + gens.parts - 1) / gens.parts;
+        a.rparts = gens.parts;
+        a.rspan = per * gens.unit;
+        a.rwaves = per;  // one wave per unit (256·nc pixels)
+        gens = Generations();
+      }
     } else if (plain && in_dtype != RTI_U8 && k == 6) {
       const int64_t groups = P * C / 4;  // 4-pixel lane groups
       for (int nc = 8; nc > 1; nc >>= 1)
@@ -1211,7 +1419,8 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
       // AUTO (no tile bits set) for fp32 at N <= 512: the 8-wave kernel on ONE 4096-pixel LDS tile
       // (16 KiB per wave and plane; c4 3.74 vs 3.93 ms for the 2048-pixel double-buffered tile,
       // profiles/r02_c4_tile_rc16_sweep.log); above N = 512 its [N][16] pinv no longer fits.
-      const bool tile_auto = (kernel & ~0xff & ~(RTI_KERNEL_NONTEMPORAL | RTI_KERNEL_ONE_LAUNCH)) == 0 && N <= 512;
+      const bool tile_auto =
+      (kernel & ~0xff & ~(RTI_KERNEL_NONTEMPORAL | RTI_KERNEL_ONE_LAUNCH | RTI_KERNEL_ROUNDS)) == 0 && N <= 512;
       const int rc0 = rc ? rc : (N <= 512 ? 8 : 4);
       int st;
       switch (in_dtype) {
@@ -1219,6 +1428,10 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
           // launch generations for the 4096-pixel tile_w kernels (AUTO, or explicit 8 waves at depth 1 /
           // 4 waves, rc >= 12: one workgroup per CU; launch_tile_w runs a 2048-pixel tile at depth 2+);
           // the other tile forms stay one launch
+          if (tile_auto && (kernel & RTI_KERNEL_ROUNDS)) {  // the tile stream: one launch, no generations
+            st = launch_tile_s(a);
+            break;
+          }
           const bool w4096 = tile_auto || (rc >= 12 && (waves == 4 || (waves == 8 && depth == 1)));
           if (w4096 && !(kernel & RTI_KERNEL_ONE_LAUNCH)) gens = tile_generations(a, 4096);
           st = launch_generations(a, es, gens, [&](const FitArgs& b) {

@@ -21,6 +21,7 @@
 // Traffic = the algorithmic bytes: every stack byte once + 4k bytes of coefficients per pixel.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "rti_internal.h"
@@ -290,9 +291,23 @@ extern "C" int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I,
   // workgroups') through its load pipeline: a tile of 1024 pixels x N <= 448 lights is only 2-7 steps, and
   // started cold each tile would wait for HBM once.  AUTO: one launch over the channels, tpw = ceil(tiles per channel / workgroups per
   // channel) with about one workgroup per CU; RTI_KERNEL_CHUNKS(n) sets tpw = n (measurement).
+  // RTI_KERNEL_TILE_DEPTH(n) (measurement): n launch generations over consecutive pixel ranges of every
+  // channel, each streamed by the same workgroups (the fp32 stream's launch generations, rti_fit.hip)
   const int64_t tpc = (P + Q8_R - 1) / Q8_R, cus = device_cus();
   const int want = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  const int parts = std::max(1, (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF);
   const int64_t wpc = cus >= C ? cus / C : 1;  // workgroups per channel: at most one per CU over all channels
-  a.tpw = want ? want : (int)((tpc + wpc - 1) / wpc);
-  return launch_q8(a);
+  const int64_t tpp = (tpc + parts - 1) / parts;  // tiles per part
+  a.tpw = want ? want : (int)((tpp + wpc - 1) / wpc);
+  if (parts == 1) return launch_q8(a);
+  int launches = 0;
+  for (int i = 0; i < parts; ++i) {
+    a.pb = i * tpp * Q8_R;
+    a.pe = std::min(P, (i + 1) * tpp * Q8_R);
+    if (a.pb >= a.pe) break;
+    const int st = launch_q8(a);
+    if (st != RTI_OK) return st;
+    note_launches(++launches);
+  }
+  return RTI_OK;
 }

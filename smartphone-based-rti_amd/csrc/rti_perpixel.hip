@@ -11,7 +11,7 @@
 // fp64 normal equations lose cond(A)²·1e-16); a pixel whose Cholesky pivots
 // show an ill-conditioned A (ne_solve) is marked and re-solved by a second,
 // refine launch (refine_*) with a streaming fp64 Givens QR of A itself
-// (qr_solve), which loses cond(A)·1e-16 like the reference's SVD; a
+// (qr_solve_wave), which loses cond(A)·1e-16 like the reference's SVD; a
 // rank-deficient A gives NaN coefficients, as the reference's division by a
 // zero singular value does.
 //
@@ -75,7 +75,7 @@ __device__ __forceinline__ void ne_finish(Normal6& ne, int N) { ne.m[tri(5, 5)] 
 // refined by Newton steps, and q̃ = dx·(1/√s) lies within a few fp64 ulps of q.  fp32 rounding looks only
 // at the low 29 bits of q's fp64 significand, so fp32(q̃) == fp32(q) unless q̃ lies within those few
 // ulps of an fp32 rounding midpoint (low 29 bits = 2^28), or the fp32 result is subnormal.  The fast form
-// folds both tests into two running minima (mid_key == 0, or |l| < FLT_MIN, flags the light: ≈1 in
+// folds both tests into two running minima (mid_key < MID_KEY_MAX, or |l| < FLT_MIN, flags the light: ≈1 in
 // 1.7·10⁷ components), and a flagged pixel is re-solved by the refine pass, whose light_dir_exact uses the
 // IEEE sqrt and divide of rti_light_dirs.  Pinned by tests/golden/ptm_perpixel_32x32_N50.npz through
 // rti_fit_perpixel_cam (test_gpu_perpixel_relight.py); the ulp budget by tools/probe/rsq_probe.hip.
@@ -85,16 +85,20 @@ __device__ __forceinline__ void ne_finish(Normal6& ne, int N) { ne.m[tri(5, 5)] 
 constexpr uint32_t MID_MARGIN = 16;
 constexpr int NEWTON = 2;
 
-// 0 iff the low 29 significand bits of q lie within MID_MARGIN of 2^28 (an fp32 rounding midpoint)
+// mid_key(q) < MID_KEY_MAX iff the low 29 significand bits of q lie within MID_MARGIN of 2^28 (an fp32
+// rounding midpoint): with lo29 = those bits, (lo << 3) + 2^31 + 8·MID_MARGIN = 8·((lo29 − 2^28 +
+// MID_MARGIN) mod 2^29) (mod 2^32; the shift drops bits 29..31 and adding 2^31 flips bit 28 of lo29),
+// one v_lshl_add_u32 per component.
+constexpr uint32_t MID_KEY_MAX = 16 * MID_MARGIN;
 __device__ __forceinline__ uint32_t mid_key(double q) {
   const uint32_t lo = (uint32_t)__double_as_longlong(q);
-  return (((lo ^ 0x10000000u) + MID_MARGIN) & 0x1FFFFFFFu) & ~(2 * MID_MARGIN - 1);
+  return (lo << 3) + (0x80000000u + 8 * MID_MARGIN);
 }
 
 struct DirCheck {
   uint32_t key = 0xFFFFFFFFu;  // min of mid_key over the pixel's light components
   float lmin = 1.0f;           // min of |l| (an fp32 subnormal or 0 result rounds on more bits)
-  __device__ __forceinline__ bool ambiguous() const { return key == 0 || !(lmin >= 0x1p-126f); }
+  __device__ __forceinline__ bool ambiguous() const { return key < MID_KEY_MAX || !(lmin >= 0x1p-126f); }
 };
 
 __device__ __forceinline__ void light_dir_fast(double dx, double dy, double dz2, float& lu, float& lv,
@@ -125,7 +129,7 @@ __device__ __forceinline__ void light_dir_exact(double dx, double dy, double dz,
 // ill-conditioned for the normal equations: a pivot kept less than ILL_RATIO of its
 // column's squared norm (the scaled cond(A)² ≳ 1/ILL_RATIO, where the normal equations
 // lose cond(A)²·1e-16 against the reference's SVD) — the caller then re-solves the pixel by
-// Givens QR of A itself (qr_solve), which loses only cond(A)·1e-16 like the SVD.
+// Givens QR of A itself (qr_solve_wave), which loses only cond(A)·1e-16 like the SVD.
 constexpr double ILL_RATIO = 1e-6;
 
 __device__ __forceinline__ bool ne_solve(const Normal6& ne, double rcond, double (&a)[6]) {
@@ -181,62 +185,114 @@ __device__ __forceinline__ bool ne_solve(const Normal6& ne, double rcond, double
 // cannot take (tests/golden/ptm_edge.npz near-collinear lights, cond(A) = 1.1e8).  `row(n, r, L)`
 // yields light n's PTM row and intensity.  Singular semantics as ne_solve: AᵀA = RᵀR, so a pivot
 // R_jj² <= rcond²·max diag(AᵀA) (rcond >= 0) or R_jj = 0 gives NaN coefficients.
-template <typename Row>
-__device__ __forceinline__ void qr_solve(int N, double rcond, Row row, double (&a)[6]) {
-  double R[21], z[6], cn[6];
+struct QR6 {
+  double R[21];  // upper 6×6 R, packed (tri)
+  double z[6];   // Qᵀ·L
+  double cn[6];  // squared column norms of A (the rcond threshold)
+};
+
+__device__ __forceinline__ void qr_zero(QR6& s) {
 #pragma unroll
-  for (int i = 0; i < 21; ++i) R[i] = 0.0;
+  for (int i = 0; i < 21; ++i) s.R[i] = 0.0;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) z[i] = cn[i] = 0.0;
-  for (int n = 0; n < N; ++n) {
-    double x[6], l;
-    row(n, x, l);
+  for (int i = 0; i < 6; ++i) s.z[i] = s.cn[i] = 0.0;
+}
+
+// rotate the row [x | l] into R (Givens, column by column; x is consumed)
+__device__ __forceinline__ void qr_rot(QR6& s, double (&x)[6], double l) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) cn[i] = fma(x[i], x[i], cn[i]);
+  for (int j = 0; j < 6; ++j) {
+    const double xj = x[j];
+    if (xj == 0.0) continue;
+    const double rjj = s.R[tri(j, j)];
+    // h = hypot(rjj, xj) and 1/h from v_rsq_f64 + two Newton steps (≈1 ulp, tools/probe/rsq_probe.hip):
+    // the rotation stays orthogonal to ~1e-16, so the QR keeps its backward stability, at a third of the
+    // latency of IEEE sqrt + divides.  Intensities and PTM rows are O(1e3) at most: h² neither overflows
+    // nor underflows.
+    const double h2 = fma(rjj, rjj, xj * xj);
+    double y = __builtin_amdgcn_rsq(h2);
+    const double hh = 0.5 * h2;
+    y = fma(y, fma(-hh * y, y, 0.5), y);
+    y = fma(y, fma(-hh * y, y, 0.5), y);
+    const double c = rjj * y, sn = xj * y;
+    s.R[tri(j, j)] = h2 * y;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const double xj = x[j];
-      if (xj == 0.0) continue;
-      const double rjj = R[tri(j, j)];
-      // h = hypot(rjj, xj) and 1/h from v_rsq_f64 + two Newton steps (≈1 ulp, tools/probe/rsq_probe.hip):
-      // the rotation stays orthogonal to ~1e-16, so the QR keeps its backward stability, at a third of the
-      // latency of IEEE sqrt + divides (the refine lane runs its N lights serially).  Intensities and PTM
-      // rows are O(1e3) at most: h² neither overflows nor underflows.
-      const double h2 = fma(rjj, rjj, xj * xj);
-      double y = __builtin_amdgcn_rsq(h2);
-      const double hh = 0.5 * h2;
-      y = fma(y, fma(-hh * y, y, 0.5), y);
-      y = fma(y, fma(-hh * y, y, 0.5), y);
-      const double c = rjj * y, sn = xj * y;
-      R[tri(j, j)] = h2 * y;
-#pragma unroll
-      for (int k = j + 1; k < 6; ++k) {
-        const double t = R[tri(j, k)];
-        R[tri(j, k)] = fma(c, t, sn * x[k]);
-        x[k] = fma(-sn, t, c * x[k]);
-      }
-      const double t = z[j];
-      z[j] = fma(c, t, sn * l);
-      l = fma(-sn, t, c * l);
+    for (int k = j + 1; k < 6; ++k) {
+      const double t = s.R[tri(j, k)];
+      s.R[tri(j, k)] = fma(c, t, sn * x[k]);
+      x[k] = fma(-sn, t, c * x[k]);
     }
+    const double t = s.z[j];
+    s.z[j] = fma(c, t, sn * l);
+    l = fma(-sn, t, c * l);
   }
+}
+
+__device__ __forceinline__ void qr_add(QR6& s, double (&x)[6], double l) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) s.cn[i] = fma(x[i], x[i], s.cn[i]);
+  qr_rot(s, x, l);
+}
+
+// TSQR merge: the rows of o's [R | z] rotated into s (QR of the stacked pair)
+__device__ __forceinline__ void qr_merge(QR6& s, const QR6& o) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double x[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) x[j] = j < i ? 0.0 : o.R[tri(i, j)];
+    qr_rot(s, x, o.z[i]);
+    s.cn[i] += o.cn[i];
+  }
+}
+
+// Singular semantics as ne_solve: AᵀA = RᵀR, so a pivot R_jj² <= rcond²·max diag(AᵀA) (rcond >= 0) or
+// R_jj = 0 gives NaN coefficients.
+__device__ __forceinline__ void qr_finish(const QR6& s, double rcond, double (&a)[6]) {
   double cmax = 0.0;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) cmax = fmax(cmax, cn[i]);
+  for (int i = 0; i < 6; ++i) cmax = fmax(cmax, s.cn[i]);
   const double thr = rcond < 0.0 ? 0.0 : rcond * sqrt(cmax);
   bool ok = true;
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
-    ok = ok && (R[tri(i, i)] > thr);
-    double s = z[i];
+    ok = ok && (s.R[tri(i, i)] > thr);
+    double t = s.z[i];
 #pragma unroll
-    for (int p = i + 1; p < 6; ++p) s -= R[tri(i, p)] * a[p];
-    a[i] = s / R[tri(i, i)];
+    for (int p = i + 1; p < 6; ++p) t -= s.R[tri(i, p)] * a[p];
+    a[i] = t / s.R[tri(i, i)];
   }
   if (!ok) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) a[i] = __builtin_nan("");
   }
+}
+
+// Least squares by Givens QR of [A | L] in fp64 (R upper 6×6 packed, z = QᵀL): backward stable in A
+// itself, so the solution carries cond(A)·1e-16 relative error — the accuracy of the reference's SVD
+// (analysis.py:295-298) for the ill-conditioned light sets the normal equations cannot take
+// (tests/golden/ptm_edge.npz near-collinear lights, cond(A) = 1.1e8).  Wave-cooperative (TSQR): lane l
+// rotates in the rows n = l, l + 64, ..., then the 64 lanes' [R | z] are merged by an xor butterfly of
+// pairwise QRs; lane 0's result is used.  `row(n, r, L)` yields light n's PTM row and intensity.
+template <typename Row>
+__device__ __forceinline__ void qr_solve_wave(int N, double rcond, Row row, double (&a)[6]) {
+  QR6 s;
+  qr_zero(s);
+  for (int n = threadIdx.x & 63; n < N; n += 64) {
+    double x[6], l;
+    row(n, x, l);
+    qr_add(s, x, l);
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    QR6 o;
+#pragma unroll
+    for (int i = 0; i < 21; ++i) o.R[i] = __shfl_xor(s.R[i], off);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) o.z[i] = __shfl_xor(s.z[i], off), o.cn[i] = __shfl_xor(s.cn[i], off);
+    qr_merge(s, o);
+  }
+  qr_finish(s, rcond, a);
 }
 
 __device__ __forceinline__ void ptm_row_d(float lu, float lv, double (&r)[6]) {
@@ -336,50 +392,84 @@ fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I
   solve_store<TC, LAYOUT>(ne, rcond, coef, P, p, chk.ambiguous());
 }
 
-// Refine launches: 256-thread blocks, one block per 4 fit waves (256 pixels), the same pixel per lane as the
-// fit; -1 past the image.  A wave whose first pixel carries no mark has nothing to redo.
-__device__ __forceinline__ int64_t refine_pixel(int64_t P) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  return p < P ? p : -1;
+// Refine launches: 256-thread blocks, one block per 4 fit waves (256 pixels), the same pixels per wave as the
+// fit.  A wave whose first pixel carries no mark has nothing to redo; otherwise the wave redoes its marked
+// pixels one after another, all 64 lanes on each (lights n = lane, lane + 64, ...; the normal equations
+// summed by an xor butterfly, so every lane holds the same sums and takes the same branch).  A lane per
+// marked pixel would run its N lights serially, each waiting for its own HBM load (≈70 µs for one
+// marked wave on c6); the wave does the same pixel in a few µs.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
 }
 
-// Refine pass of fit_perpixel_cam, one lane per marked pixel: EXACT pixels are re-accumulated with the
-// IEEE light vectors (light_dir_exact) and solved as in the fit (falling through to QR if ill-conditioned),
-// QR pixels go straight to the Givens QR of their exact rows.  A scan of one coefficient per pixel when
-// nothing is marked; a marked lane runs its N lights serially (tens of µs at N = 100).
+template <typename RowF>
+__device__ __forceinline__ void ne_wave(int N, RowF row, Normal6& ne) {
+  ne_zero(ne);
+  for (int n = threadIdx.x & 63; n < N; n += 64) {
+    float lu, lv;
+    double L;
+    row(n, lu, lv, L);
+    ne_add(ne, lu, lv, L);
+  }
+#pragma unroll
+  for (int i = 0; i < 21; ++i) ne.m[i] = wave_sum(ne.m[i]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) ne.b[i] = wave_sum(ne.b[i]);
+  ne_finish(ne, N);
+}
+
+// The marked pixels of this wave (mask over lanes) and their marks; none when the wave's flag is clear.
+template <typename TC, int LAYOUT>
+__device__ __forceinline__ uint64_t refine_marks(const TC* coef, int64_t P, int64_t& w0, int& mark) {
+  w0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);
+  mark = MARK_NONE;
+  if (w0 >= P || mark_of<TC, LAYOUT>(coef, P, w0) == MARK_NONE) return 0;  // wave-uniform
+  const int64_t p = w0 + (threadIdx.x & 63);
+  if (p < P) mark = mark_of<TC, LAYOUT>(coef, P, p);
+  return __ballot(mark != MARK_NONE);
+}
+
+// Refine pass of fit_perpixel_cam: EXACT pixels are re-accumulated with the IEEE light vectors
+// (light_dir_exact) and solved as in the fit (falling through to QR if ill-conditioned); QR pixels go
+// straight to the Givens QR of their exact rows.
 template <typename T, typename TC, int LAYOUT>
 __global__ void __launch_bounds__(256)
 refine_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
            double x0, double y0, double rcond, TC* __restrict__ coef) {
   const int64_t P = (int64_t)H * W;
-  const int64_t p = refine_pixel(P);
-  if (p < 0 || mark_of<TC, LAYOUT>(coef, P, p & ~(int64_t)63) == MARK_NONE) return;  // the wave's flag
-  const int mark = mark_of<TC, LAYOUT>(coef, P, p);
-  if (mark == MARK_NONE) return;
-  const double px = x0 + (double)(p % W);
-  const double py = y0 + (double)(p / W);
-  const T* __restrict__ src = I + p;
-  double a[6];
-  bool qr = mark == MARK_QR;
-  if (!qr) {
-    Normal6 ne;
-    ne_zero(ne);
-    for (int n = 0; n < N; ++n) {
-      float lu, lv;
+  int64_t w0;
+  int mark;
+  uint64_t m = refine_marks<TC, LAYOUT>(coef, P, w0, mark);
+  const int lane = threadIdx.x & 63;
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    const int64_t q = w0 + l;
+    const int mk = __shfl(mark, l);
+    const double px = x0 + (double)(q % W);
+    const double py = y0 + (double)(q / W);
+    const T* __restrict__ src = I + q;
+    auto row = [&](int n, float& lu, float& lv, double& L) {
       light_dir_exact(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv);
-      ne_add(ne, lu, lv, ld_d(src + (int64_t)n * lstride));
-    }
-    ne_finish(ne, N);
-    qr = ne_solve(ne, rcond, a);
-  }
-  if (qr)
-    qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
-      float lu, lv;
-      light_dir_exact(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cams[3 * n + 2], lu, lv);
-      ptm_row_d(lu, lv, r);
       L = ld_d(src + (int64_t)n * lstride);
-    }, a);
-  store_coef<TC, LAYOUT>(coef, P, p, a);
+    };
+    double a[6];
+    bool qr = mk == MARK_QR;
+    if (!qr) {
+      Normal6 ne;
+      ne_wave(N, row, ne);
+      qr = ne_solve(ne, rcond, a);
+    }
+    if (qr)
+      qr_solve_wave(N, rcond, [&](int n, double (&r)[6], double& L) {
+        float lu, lv;
+        row(n, lu, lv, L);
+        ptm_row_d(lu, lv, r);
+      }, a);
+    if (lane == 0) store_coef<TC, LAYOUT>(coef, P, q, a);
+  }
 }
 
 template <typename T, typename TC, int LAYOUT>
@@ -401,26 +491,33 @@ template <typename T, typename TC, int LAYOUT>
 __global__ void __launch_bounds__(256)
 refine_dirs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N,
                int64_t P, double rcond, TC* __restrict__ coef) {
-  const int64_t p = refine_pixel(P);
-  if (p < 0 || mark_of<TC, LAYOUT>(coef, P, p & ~(int64_t)63) == MARK_NONE) return;  // the wave's flag
-  const int mark = mark_of<TC, LAYOUT>(coef, P, p);
-  if (mark == MARK_NONE) return;
-  const int64_t base = p * N;
-  double a[6];
-  bool qr = mark == MARK_QR;
-  if (!qr) {  // the wave's first pixel (or a pixel redone from the start): the fit's own normal equations
-    Normal6 ne;
-    ne_zero(ne);
-    for (int n = 0; n < N; ++n) ne_add(ne, lu[base + n], lv[base + n], ld_d(I + base + n));
-    ne_finish(ne, N);
-    qr = ne_solve(ne, rcond, a);
+  int64_t w0;
+  int mark;
+  uint64_t m = refine_marks<TC, LAYOUT>(coef, P, w0, mark);
+  const int lane = threadIdx.x & 63;
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    const int64_t q = w0 + l, base = q * N;
+    const int mk = __shfl(mark, l);
+    double a[6];
+    bool qr = mk == MARK_QR;
+    if (!qr) {  // the wave's first pixel (or a pixel redone from the start): the fit's own normal equations
+      Normal6 ne;
+      ne_wave(N, [&](int n, float& u, float& v, double& L) {
+        u = lu[base + n];
+        v = lv[base + n];
+        L = ld_d(I + base + n);
+      }, ne);
+      qr = ne_solve(ne, rcond, a);
+    }
+    if (qr)
+      qr_solve_wave(N, rcond, [&](int n, double (&r)[6], double& L) {
+        ptm_row_d(lu[base + n], lv[base + n], r);
+        L = ld_d(I + base + n);
+      }, a);
+    if (lane == 0) store_coef<TC, LAYOUT>(coef, P, q, a);
   }
-  if (qr)
-    qr_solve(N, rcond, [&](int n, double (&r)[6], double& L) {
-      ptm_row_d(lu[base + n], lv[base + n], r);
-      L = ld_d(I + base + n);
-    }, a);
-  store_coef<TC, LAYOUT>(coef, P, p, a);
 }
 
 // compute_intensities' light vectors (analysis.py:225-231); lane = (pixel, camera),

@@ -45,6 +45,7 @@ RTI_KERNEL_NT_STORE = 0x400
 RTI_KERNEL_STAGE = 0x800
 RTI_KERNEL_ROTATE = 0x10000000  # measurement variant: per-wave rotated light order (AUTO PTM-6 fp32)
 RTI_KERNEL_ONE_LAUNCH = 0x20000000  # measurement variant: AUTO without launch generations
+RTI_KERNEL_ROUNDS = 0x40000000  # measurement variant: AUTO generations as rounds of one launch
 RTI_KERNEL_CHUNKS_SHIFT = 12  # VALU chunks per lane in bits 12-15 (0 = AUTO)
 RTI_KERNEL_TILE_PLANES_SHIFT = 16  # TILE kernel: light planes per wave and step in bits 16-19 (0 = 2)
 RTI_KERNEL_TILE_DEPTH_SHIFT = 20  # TILE kernel: tiles in the LDS ring in bits 20-23 (0 = 2)

@@ -302,6 +302,13 @@ def test_launch_generations_bit_identical(cuda, basis, N, C, layout):
     torch.cuda.synchronize()
     assert not torch.isnan(a).any()
     assert torch.equal(a, b)
+    # the same generations as rounds of one launch (RTI_KERNEL_ROUNDS: the VALU rounds kernel for PTM-6, the
+    # tile stream for HSH-16): same per-pixel arithmetic, so the same bits
+    r = torch.full(shape, float("nan"), device=cuda)
+    rti.fit_shared_into(pv, I, r, k=k, layout=layout, flags=L.RTI_KERNEL_ROUNDS)
+    assert int(L.lib().rti_last_launch_count()) == 1
+    torch.cuda.synchronize()
+    assert torch.equal(r, b)
     # and against the fp64 oracle on sampled pixels of the last channel (parts' boundaries included)
     px = np.unique(np.concatenate([np.random.default_rng(5).integers(0, P, 512), [0, P - 1, P // 5, P // 5 - 1]]))
     ref = o.fit_shared(I[-1][:, torch.as_tensor(px, device=cuda)].cpu().numpy(), o.pinv_shared(basis, lu, lv))

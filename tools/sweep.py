@@ -46,6 +46,7 @@ def main():
     if args.in_dtype != "f32":  # integer-valued 0..255 stacks, as the reference's V channel
         I = I.to(torch.uint8 if args.in_dtype == "u8" else torch.int32)
     pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=dev)
+    op_dev = torch.as_tensor(rti.q8_operator(rti.pinv(lu, lv, basis)), device=dev) if args.in_dtype == "u8" else None
     coefs = {"pixel": torch.empty((C, P, k), device=dev), "planar": torch.empty((C, k, P), device=dev)}
     variants = []
     for v in args.variants.split(","):
@@ -54,7 +55,8 @@ def main():
         fl = (rti._lib.RTI_KERNEL_NONTEMPORAL if "nt" in opts else 0) | \
              (rti._lib.RTI_KERNEL_PINV_LDS if "lds" in opts else 0) | \
              (rti._lib.RTI_KERNEL_NT_STORE if "nts" in opts else 0) | (rti._lib.RTI_KERNEL_STAGE if "stage" in opts else 0) | \
-             (rti._lib.RTI_KERNEL_ONE_LAUNCH if "one" in opts else 0)
+             (rti._lib.RTI_KERNEL_ONE_LAUNCH if "one" in opts else 0) | \
+             (rti._lib.RTI_KERNEL_ROUNDS if "rounds" in opts else 0)
         for o in opts:  # c<n>: chunks per lane (rti.h RTI_KERNEL_CHUNKS)
             if o[:1] == "c" and o[1:].isdigit():
                 fl |= int(o[1:]) << 12
@@ -119,6 +121,8 @@ def main():
         elif kern == "pfit":
             probe.probe_fit6(ctypes.c_void_p(pv.data_ptr()), ctypes.c_void_p(I.data_ptr()), N, P,
                              ctypes.c_void_p(coefs["pixel"].data_ptr()), int(layout), ctypes.c_void_p(stream.cuda_stream))
+        elif kern == "q8":
+            rti.api.fit_q8_into(op_dev, I, coefs[layout], k=k, layout=layout, flags=fl)
         else:
             rti.fit_shared_into(pv, I, coefs[layout], k=k, layout=layout, kernel=kern, flags=fl)
 
@@ -127,7 +131,7 @@ def main():
     for name, kern, layout, fl in variants:  # warm-up
         for _ in range(3):
             launch(kern, layout, fl)
-        if kern in ("valu", "mfma", "tile", "auto"):
+        if kern in ("valu", "mfma", "tile", "auto", "q8"):
             got = coefs[layout] if layout == "pixel" else coefs[layout].transpose(1, 2)
             got = got.double()
             if ref is None:
@@ -143,7 +147,8 @@ def main():
             b.record(stream)
             times[name].append((a, b))
     torch.cuda.synchronize()
-    alg = 4.0 * P * N * C + 4.0 * P * k * C
+    es = I.element_size()
+    alg = es * P * N * C + 4.0 * P * k * C
     res = {}
     for name, *rest in variants:
         ms = np.array([a.elapsed_time(b) for a, b in times[name]])
