@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <type_traits>
 
 #include "rti_basis.h"
 #include "rti_internal.h"
@@ -72,46 +74,56 @@ __device__ __forceinline__ void ne_finish(Normal6& ne, int N) { ne.m[tri(5, 5)] 
 // (:230-231), BIT-EXACT with the reference's arrays at the cost of an rsq: the reference rounds
 // s = (dx² + dy²) + dz² op by op, n = sqrt(s) and q = dx / n correctly (IEEE fp64), then q to fp32.
 // Here s = fma(dx, dx, fma(dy, dy, dz²)) (within 2 ulps of the reference's s), 1/√s is the v_rsq_f64 seed
-// refined by Newton steps, and q̃ = dx·(1/√s) lies within a few fp64 ulps of q.  fp32 rounding looks only
-// at the low 29 bits of q's fp64 significand, so fp32(q̃) == fp32(q) unless q̃ lies within those few
-// ulps of an fp32 rounding midpoint (low 29 bits = 2^28), or the fp32 result is subnormal.  The fast form
-// folds both tests into two running minima (mid_key < MID_KEY_MAX, or |l| < FLT_MIN, flags the light: ≈1 in
-// 1.7·10⁷ components), and a flagged pixel is re-solved by the refine pass, whose light_dir_exact uses the
-// IEEE sqrt and divide of rti_light_dirs.  Pinned by tests/golden/ptm_perpixel_32x32_N50.npz through
-// rti_fit_perpixel_cam (test_gpu_perpixel_relight.py); the ulp budget by tools/probe/rsq_probe.hip.
-// fp64 ulps of q: |q̃ − q_ref| <= ~4.5 ulps (s: two fma roundings vs the reference's four, <= 4 ulps of s
-// -> 2 of 1/√s; rsq + 2 Newton steps 0.99 ulp, tools/probe/rsq_probe.hip; the product 0.5; the
-// reference's sqrt and divide 0.5 each), so a margin of 16 leaves a factor 3.5
-constexpr uint32_t MID_MARGIN = 16;
-constexpr int NEWTON = 2;
+// refined by ONE Newton step, and q̃ = dx·(1/√s) lies within ~200 fp64 ulps of q.  fp32 rounding looks only
+// at the low 29 bits of q's fp64 significand, so fp32(q̃) == fp32(q) unless q̃ lies within those ulps of an
+// fp32 rounding midpoint (low 29 bits = 2^28), or the fp32 result is subnormal.  The fast form folds both
+// tests into two running minima (mid_key < MID_KEY_MAX, or |l| < FLT_MIN, flags the light: ≈1 in 5·10⁵
+// components, a few thousand pixels of a 4K image), and a flagged pixel is re-solved by the refine pass,
+// whose light_dir_exact uses the IEEE sqrt and divide of rti_light_dirs.  Pinned by
+// tests/golden/ptm_perpixel_32x32_N50.npz through rti_fit_perpixel_cam (test_gpu_perpixel_relight.py).
+// Ulp budget of q̃ (tools/probe/rsq_probe.hip, profiles/r03_rsq_probe.log: v_rsq_f64 ≤ 2.46e8 ulps measured,
+// 2^29 documented; one Newton step ≤ 19.8 ulps measured, ≤ 1.5·(2^-23)² relative = 192 ulps from the
+// documented seed; two steps 0.99): s two fma roundings vs the reference's four (≤ 4 ulps of s -> 2 of
+// 1/√s), the product 0.5, the reference's sqrt and divide 0.5 each: ≤ 196 ulps, so a margin of 512 leaves
+// a factor 2.6.  One Newton step instead of two saves 3 of the ≈57 VALU ops per pixel·light; the extra
+// flagged pixels cost the wave-cooperative refine a few µs.
+// NW Newton steps on the rsq seed, and the midpoint margin that covers the resulting ulp budget: one step
+// (≤ 196 ulps) with a margin of 512, or two steps (≤ 4.5 ulps: rsq + 2 Newton steps 0.99 ulp, the rest as
+// above) with a margin of 16.  AUTO uses one step (profiles/r03_c6_variants_sweep.log).
+template <int NW>
+constexpr uint32_t mid_margin() { return NW >= 2 ? 16 : 512; }
 
-// mid_key(q) < MID_KEY_MAX iff the low 29 significand bits of q lie within MID_MARGIN of 2^28 (an fp32
-// rounding midpoint): with lo29 = those bits, (lo << 3) + 2^31 + 8·MID_MARGIN = 8·((lo29 − 2^28 +
-// MID_MARGIN) mod 2^29) (mod 2^32; the shift drops bits 29..31 and adding 2^31 flips bit 28 of lo29),
-// one v_lshl_add_u32 per component.
-constexpr uint32_t MID_KEY_MAX = 16 * MID_MARGIN;
+// mid_key(q) < 16·margin iff the low 29 significand bits of q lie within `margin` of 2^28 (an fp32 rounding
+// midpoint): with lo29 = those bits, (lo << 3) + 2^31 + 8·margin = 8·((lo29 − 2^28 + margin) mod 2^29)
+// (mod 2^32; the shift drops bits 29..31 and adding 2^31 flips bit 28 of lo29), one v_lshl_add_u32 per
+// component.
+template <int NW>
 __device__ __forceinline__ uint32_t mid_key(double q) {
   const uint32_t lo = (uint32_t)__double_as_longlong(q);
-  return (lo << 3) + (0x80000000u + 8 * MID_MARGIN);
+  return (lo << 3) + (0x80000000u + 8 * mid_margin<NW>());
 }
 
+template <int NW>
 struct DirCheck {
   uint32_t key = 0xFFFFFFFFu;  // min of mid_key over the pixel's light components
   float lmin = 1.0f;           // min of |l| (an fp32 subnormal or 0 result rounds on more bits)
-  __device__ __forceinline__ bool ambiguous() const { return key < MID_KEY_MAX || !(lmin >= 0x1p-126f); }
+  __device__ __forceinline__ bool ambiguous() const {
+    return key < 16 * mid_margin<NW>() || !(lmin >= 0x1p-126f);
+  }
 };
 
+template <int NW>
 __device__ __forceinline__ void light_dir_fast(double dx, double dy, double dz2, float& lu, float& lv,
-                                               DirCheck& chk) {
+                                               DirCheck<NW>& chk) {
   const double s = fma(dx, dx, fma(dy, dy, dz2));
   double y = __builtin_amdgcn_rsq(s);
   const double h = 0.5 * s;
 #pragma unroll
-  for (int i = 0; i < NEWTON; ++i) y = fma(y, fma(-h * y, y, 0.5), y);
+  for (int i = 0; i < NW; ++i) y = fma(y, fma(-h * y, y, 0.5), y);
   const double qx = dx * y, qy = dy * y;
   lu = (float)qx;
   lv = (float)qy;
-  chk.key = min(chk.key, min(mid_key(qx), mid_key(qy)));
+  chk.key = min(chk.key, min(mid_key<NW>(qx), mid_key<NW>(qy)));
   chk.lmin = fminf(chk.lmin, fminf(fabsf(lu), fabsf(lv)));
 }
 
@@ -367,11 +379,36 @@ __device__ __forceinline__ int mark_of(const TC* coef, int64_t P, int64_t p) {
   return u == Mark<TC>::exact ? MARK_EXACT : (u == Mark<TC>::qr ? MARK_QR : MARK_NONE);
 }
 
-template <typename T, typename TC, int LAYOUT>
+// The fused fit: each light enters the normal equations as soon as its fast light vector is formed, and the
+// DirCheck of each group of 4 lights is tested once.  A lane whose group holds an ambiguous component (≈1 in
+// 5·10⁵ components, so a wave takes the branch about once in 40 groups of its 25) recomputes the group's fast
+// vectors (deterministic: the same bits) and replaces every one that differs from the reference's IEEE vector
+// (light_dir_exact) by subtracting its row and adding the exact one.  Every light vector in the final normal
+// equations is the reference's, bit for bit (the sums carry one extra rounding per replaced row, ≈1e-16
+// relative), and only ill-conditioned pixels (MARK_QR) are left to the refine pass.  The fix-up recomputes
+// rather than keeps the group's vectors so the hot loop stays within its 80-VGPR budget (6 waves per SIMD);
+// a whole-pixel redo in the same place measured 1.71 ms against 1.51 ms + a 96 µs refine pass.
+__device__ __forceinline__ void ne_sub(Normal6& ne, float lu, float lv, double L) {
+  const double r[5] = {(double)(lu * lu), (double)(lv * lv), (double)(lu * lv), (double)lu, (double)lv};
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+#pragma unroll
+    for (int j = i; j < 5; ++j) ne.m[tri(i, j)] = fma(-r[i], r[j], ne.m[tri(i, j)]);
+    ne.m[tri(i, 5)] -= r[i];
+    ne.b[i] = fma(-r[i], L, ne.b[i]);
+  }
+  ne.b[5] -= L;
+}
+
+// VAR (measurement switch RTI_PERPIXEL_VARIANT, default 2): 0 = two Newton steps, an ambiguous pixel marked
+// for the refine pass; 1 = one step, marked; 2 = one step, fixed up in place per group of 4 lights;
+// 3 = 2 at 5 waves per SIMD (96 VGPRs: the fix-up's IEEE temporaries without spills).
+template <typename T, typename TC, int LAYOUT, int VAR>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(6)))
+__attribute__((amdgpu_waves_per_eu(VAR == 3 ? 5 : 6)))
 fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
                  double x0, double y0, double rcond, TC* __restrict__ coef) {
+  constexpr int NW = VAR == 0 ? 2 : 1;
   const int64_t P = (int64_t)H * W;
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
@@ -379,25 +416,63 @@ fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I
   const double py = y0 + (double)(p / W);
   Normal6 ne;
   ne_zero(ne);
-  DirCheck chk;
   const uint32_t po = (uint32_t)(p * (int64_t)sizeof(T));  // per-lane byte offset into each plane (< 2^32: launcher)
-#pragma unroll 4
-  for (int n = 0; n < N; ++n) {
-    float lu, lv;  // cams: wave-uniform -> scalar loads; the plane base is wave-uniform too
+  auto plane = [&](int n) {  // cams and the plane base are wave-uniform: scalar loads
+    return ld_d(reinterpret_cast<const T*>(reinterpret_cast<const char*>(I + (int64_t)n * lstride) + po));
+  };
+  auto light = [&](int n, DirCheck<NW>& chk) {
+    float lu, lv;
     const double cz = cams[3 * n + 2];
-    light_dir_fast(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cz * cz, lu, lv, chk);
-    ne_add(ne, lu, lv, ld_d(reinterpret_cast<const T*>(reinterpret_cast<const char*>(I + (int64_t)n * lstride) + po)));
+    light_dir_fast<NW>(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cz * cz, lu, lv, chk);
+    ne_add(ne, lu, lv, plane(n));
+  };
+  if constexpr (VAR < 2) {
+    DirCheck<NW> chk;
+#pragma unroll 4
+    for (int n = 0; n < N; ++n) light(n, chk);
+    ne_finish(ne, N);
+    solve_store<TC, LAYOUT>(ne, rcond, coef, P, p, chk.ambiguous());
+  } else {
+    auto fix = [&](int n0, int G) {
+#pragma clang loop unroll(disable)
+      for (int u = 0; u < G; ++u) {
+        const int n = n0 + u;
+        const double cz = cams[3 * n + 2];
+        float fu, fv, eu, ev;
+        DirCheck<NW> unused;
+        light_dir_fast<NW>(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cz * cz, fu, fv, unused);
+        light_dir_exact(cams[3 * n + 0] - px, cams[3 * n + 1] - py, cz, eu, ev);
+        if (__float_as_uint(fu) != __float_as_uint(eu) || __float_as_uint(fv) != __float_as_uint(ev)) {
+          const double L = plane(n);
+          ne_sub(ne, fu, fv, L);
+          ne_add(ne, eu, ev, L);
+        }
+      }
+    };
+    int n = 0;
+    for (; n + 4 <= N; n += 4) {
+      DirCheck<NW> chk;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) light(n + u, chk);
+      if (__builtin_expect(chk.ambiguous(), 0)) fix(n, 4);
+    }
+    for (; n < N; ++n) {
+      DirCheck<NW> chk;
+      light(n, chk);
+      if (__builtin_expect(chk.ambiguous(), 0)) fix(n, 1);
+    }
+    ne_finish(ne, N);
+    solve_store<TC, LAYOUT>(ne, rcond, coef, P, p);
   }
-  ne_finish(ne, N);
-  solve_store<TC, LAYOUT>(ne, rcond, coef, P, p, chk.ambiguous());
 }
 
-// Refine launches: 256-thread blocks, one block per 4 fit waves (256 pixels), the same pixels per wave as the
-// fit.  A wave whose first pixel carries no mark has nothing to redo; otherwise the wave redoes its marked
-// pixels one after another, all 64 lanes on each (lights n = lane, lane + 64, ...; the normal equations
-// summed by an xor butterfly, so every lane holds the same sums and takes the same branch).  A lane per
-// marked pixel would run its N lights serially, each waiting for its own HBM load (≈70 µs for one
-// marked wave on c6); the wave does the same pixel in a few µs.
+// Refine launches (refine_grid): wave gw looks after the 64 fit waves (4096 pixels) [64·gw, 64·gw + 64): lane i
+// reads the flag of fit wave 64·gw + i (its first pixel's first coefficient), so the pass reads one value
+// per 64 pixels and dispatches one workgroup per 16 384 pixels.  A flagged fit wave's 64 marks are read
+// by the 64 lanes and its marked pixels redone one after another, all 64 lanes on each (lights n = lane,
+// lane + 64, ...; the normal equations summed by an xor butterfly, so every lane holds the same sums and
+// takes the same branch).  A lane per marked pixel would run its N lights serially, each waiting for its
+// own HBM load (≈70 µs for one marked wave on c6); the wave does the same pixel in a few µs.
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -420,34 +495,41 @@ __device__ __forceinline__ void ne_wave(int N, RowF row, Normal6& ne) {
   ne_finish(ne, N);
 }
 
-// The marked pixels of this wave (mask over lanes) and their marks; none when the wave's flag is clear.
-template <typename TC, int LAYOUT>
-__device__ __forceinline__ uint64_t refine_marks(const TC* coef, int64_t P, int64_t& w0, int& mark) {
-  w0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);
-  mark = MARK_NONE;
-  if (w0 >= P || mark_of<TC, LAYOUT>(coef, P, w0) == MARK_NONE) return 0;  // wave-uniform
-  const int64_t p = w0 + (threadIdx.x & 63);
-  if (p < P) mark = mark_of<TC, LAYOUT>(coef, P, p);
-  return __ballot(mark != MARK_NONE);
+// Calls solve(q, mark) for every marked pixel q of the flagged fit waves this wave looks after (wave-uniform).
+template <typename TC, int LAYOUT, typename F>
+__device__ __forceinline__ void refine_scan(const TC* coef, int64_t P, F&& solve) {
+  const int lane = threadIdx.x & 63;
+  const int64_t fw0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64, nfw = (P + 63) / 64;
+  const bool flagged = fw0 + lane < nfw && mark_of<TC, LAYOUT>(coef, P, (fw0 + lane) * 64) != MARK_NONE;
+  uint64_t fm = __ballot(flagged);
+  while (fm) {
+    const int64_t w0 = (fw0 + __builtin_ctzll(fm)) * 64;
+    fm &= fm - 1;
+    const int64_t p = w0 + lane;
+    const int mark = p < P ? mark_of<TC, LAYOUT>(coef, P, p) : MARK_NONE;
+    uint64_t m = __ballot(mark != MARK_NONE);
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      solve(w0 + l, __shfl(mark, l));
+    }
+  }
 }
 
-// Refine pass of fit_perpixel_cam: EXACT pixels are re-accumulated with the IEEE light vectors
-// (light_dir_exact) and solved as in the fit (falling through to QR if ill-conditioned); QR pixels go
-// straight to the Givens QR of their exact rows.
+// one refine wave per 64 fit waves
+inline dim3 refine_grid(int64_t P) { return dim3((unsigned)(((P + 63) / 64 + 255) / 256)); }
+
+// Refine pass of fit_perpixel_cam: QR pixels (ill-conditioned) are solved by the Givens QR of their exact
+// rows; an EXACT mark is a wave's flag on its first pixel, which is re-accumulated with the IEEE light
+// vectors (light_dir_exact, the vectors the fit used) and solved as in the fit (falling through to QR if
+// ill-conditioned).
 template <typename T, typename TC, int LAYOUT>
 __global__ void __launch_bounds__(256)
 refine_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
            double x0, double y0, double rcond, TC* __restrict__ coef) {
   const int64_t P = (int64_t)H * W;
-  int64_t w0;
-  int mark;
-  uint64_t m = refine_marks<TC, LAYOUT>(coef, P, w0, mark);
   const int lane = threadIdx.x & 63;
-  while (m) {
-    const int l = __builtin_ctzll(m);
-    m &= m - 1;
-    const int64_t q = w0 + l;
-    const int mk = __shfl(mark, l);
+  refine_scan<TC, LAYOUT>(coef, P, [&](int64_t q, int mk) {
     const double px = x0 + (double)(q % W);
     const double py = y0 + (double)(q / W);
     const T* __restrict__ src = I + q;
@@ -469,7 +551,7 @@ refine_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int 
         ptm_row_d(lu, lv, r);
       }, a);
     if (lane == 0) store_coef<TC, LAYOUT>(coef, P, q, a);
-  }
+  });
 }
 
 template <typename T, typename TC, int LAYOUT>
@@ -491,15 +573,9 @@ template <typename T, typename TC, int LAYOUT>
 __global__ void __launch_bounds__(256)
 refine_dirs(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N,
                int64_t P, double rcond, TC* __restrict__ coef) {
-  int64_t w0;
-  int mark;
-  uint64_t m = refine_marks<TC, LAYOUT>(coef, P, w0, mark);
   const int lane = threadIdx.x & 63;
-  while (m) {
-    const int l = __builtin_ctzll(m);
-    m &= m - 1;
-    const int64_t q = w0 + l, base = q * N;
-    const int mk = __shfl(mark, l);
+  refine_scan<TC, LAYOUT>(coef, P, [&](int64_t q, int mk) {
+    const int64_t base = q * N;
     double a[6];
     bool qr = mk == MARK_QR;
     if (!qr) {  // the wave's first pixel (or a pixel redone from the start): the fit's own normal equations
@@ -517,7 +593,7 @@ refine_dirs(const float* __restrict__ lu, const float* __restrict__ lv, const T*
         L = ld_d(I + base + n);
       }, a);
     if (lane == 0) store_coef<TC, LAYOUT>(coef, P, q, a);
-  }
+  });
 }
 
 // compute_intensities' light vectors (analysis.py:225-231); lane = (pixel, camera),
@@ -545,9 +621,14 @@ template <typename T, typename TC, int LAYOUT>
 void launch_cam(const double* cams, int N, const void* I, int H, int W, int64_t ls, double x0, double y0,
                 double rcond, void* coef, hipStream_t s) {
   const int64_t P = (int64_t)H * W;
-  hipLaunchKernelGGL((fit_perpixel_cam<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N,
-                     static_cast<const T*>(I), H, W, ls, x0, y0, rcond, static_cast<TC*>(coef));
-  hipLaunchKernelGGL((refine_cam<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N,
+  const char* ev = getenv("RTI_PERPIXEL_VARIANT");  // measurement switch, read per call (A/B in one process)
+  const int var = ev ? atoi(ev) : 2;
+  auto kern = var == 0 ? fit_perpixel_cam<T, TC, LAYOUT, 0>
+             : var == 1 ? fit_perpixel_cam<T, TC, LAYOUT, 1>
+             : var == 3 ? fit_perpixel_cam<T, TC, LAYOUT, 3> : fit_perpixel_cam<T, TC, LAYOUT, 2>;
+  hipLaunchKernelGGL(kern, dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N, static_cast<const T*>(I), H, W, ls, x0,
+                     y0, rcond, static_cast<TC*>(coef));
+  hipLaunchKernelGGL((refine_cam<T, TC, LAYOUT>), refine_grid(P), dim3(256), 0, s, cams, N,
                      static_cast<const T*>(I), H, W, ls, x0, y0, rcond, static_cast<TC*>(coef));
 }
 
@@ -574,7 +655,7 @@ void launch_dirs(const float* lu, const float* lv, const void* I, int N, int64_t
                  hipStream_t s) {
   hipLaunchKernelGGL((fit_perpixel_dirs<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, lu, lv,
                      static_cast<const T*>(I), N, P, rcond, static_cast<TC*>(coef));
-  hipLaunchKernelGGL((refine_dirs<T, TC, LAYOUT>), dim3(grid_1d(P, 256)), dim3(256), 0, s, lu, lv,
+  hipLaunchKernelGGL((refine_dirs<T, TC, LAYOUT>), refine_grid(P), dim3(256), 0, s, lu, lv,
                      static_cast<const T*>(I), N, P, rcond, static_cast<TC*>(coef));
 }
 

@@ -37,6 +37,16 @@ def test_stub_ptm_fit_and_residual(cuda):
     assert np.isfinite(rms) and res.shape == I.shape[1:]
 
 
+def test_stub_ptm_fit_u8(cuda):
+    ns = _stub_namespace()
+    d = golden("ptm_shared_256x256_N20.npz")
+    I = torch.as_tensor(d["I"], device=cuda).to(torch.uint8)  # the golden stack is integer 0..255
+    assert torch.equal(I.float(), torch.as_tensor(d["I"].astype(np.float32), device=cuda))
+    coef = ns["ptm_fit_u8"](I, d["lu"], d["lv"]).cpu().numpy()
+    err, ok = coef_close(coef.reshape(-1, 6), d["coef"].reshape(-1, 6))
+    assert ok, err
+
+
 def test_stub_rbf_tables(cuda):
     ns = _stub_namespace()
     d = golden("rbf_perpixel_4x4_N50.npz")
