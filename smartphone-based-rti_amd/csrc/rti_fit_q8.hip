@@ -65,7 +65,7 @@ __device__ __forceinline__ void q8_store(float* __restrict__ dst, int64_t P, int
   }
 }
 
-template <int K, int LAYOUT>
+template <int K, int LAYOUT, bool STAGE>
 __global__ void __launch_bounds__(64 * Q8_W)
 fit_q8(const unsigned char* __restrict__ op, int N, const unsigned char* __restrict__ I, int64_t pb, int64_t pe,
        int tpw, int64_t P, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
@@ -143,29 +143,58 @@ fit_q8(const unsigned char* __restrict__ op, int N, const unsigned char* __restr
   float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
   // acc[c][d][r] = digit d's sum for coefficient 4g + r of pixel t0 + 128·wave + 16c + (lane & 15); the stores
   // of tile i are issued while the loads of tile i + 1 are in flight
-  auto finish = [&](int ti) {
+  // Pixel-major rows leave through LDS: the wave parks its 128 pixels' rows (128·K floats, contiguous in
+  // coef) in ITS OWN rows 8·wave .. 8·wave + 7 of the tile buffer that is free at that point (no other wave
+  // writes them; every wave finished reading that buffer before the last barrier), reads them back 16 B per
+  // lane at a 1 KiB stride and stores whole 1 KiB runs per instruction (the direct form writes 8-B pieces of
+  // 24-B rows from half the lanes).  `fb` = the free tile buffer.  STAGE = RTI_KERNEL_STAGE (measurement).
+  auto finish = [&](int ti, int fb) {
     const int64_t t0 = tile_px(ti);
-    if (4 * g < K) {
-      double sc[4];
-      int cr[4][Q8_DIGITS];
+    double sc[4];
+    int cr[4][Q8_DIGITS];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sc[r] = scale[4 * g + r];
+    for (int r = 0; r < 4; ++r) {
+      sc[r] = 4 * g + r < K ? scale[4 * g + r] : 0.0;
 #pragma unroll
-        for (int d = 0; d < Q8_DIGITS; ++d) cr[r][d] = corr[(4 * g + r) * Q8_DIGITS + d];
+      for (int d = 0; d < Q8_DIGITS; ++d) cr[r][d] = 4 * g + r < K ? corr[(4 * g + r) * Q8_DIGITS + d] : 0;
+    }
+    auto value = [&](int c, int r) {
+      double sm = (double)(acc[c][0][r] + cr[r][0]);  // exact: |Σ| < 2^53 for N < 2^18
+#pragma unroll
+      for (int d = 1; d < Q8_DIGITS; ++d) sm = fma(sm, 128.0, (double)(acc[c][d][r] + cr[r][d]));
+      return (float)(sm * sc[r]);
+    };
+    if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && STAGE) {
+      float* __restrict__ st = reinterpret_cast<float*>(tile + fb * (Q8_STEP * Q8_RS) + (8 * wave) * Q8_RS);
+      if (4 * g < K) {
+#pragma unroll
+        for (int c = 0; c < Q8_G; ++c) {
+          float* row = st + (16 * c + (lane & 15)) * K + 4 * g;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (4 * g + r < K) row[r] = value(c, r);
+        }
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int CH = Q8_WPX * K / 4;  // 16-B chunks of the wave's rows: 192 (K = 6) .. 512 (K = 16)
+      const int64_t pw = t0 + Q8_WPX * wave;
+      float* __restrict__ wdst = dst + pw * K;
+#pragma unroll
+      for (int i = lane; i < CH; i += 64) {
+        // a chunk never straddles a 16-pixel block (16·K floats = 4K chunks), and pe is 16-pixel aligned
+        if (pw + (4 * i) / K < pe)
+          *reinterpret_cast<floatx4*>(wdst + 4 * i) = *reinterpret_cast<const floatx4*>(st + 4 * i);
+      }
+    } else if (4 * g < K) {
 #pragma unroll
       for (int c = 0; c < Q8_G; ++c) {
         const int64_t p = t0 + Q8_WPX * wave + 16 * c + (lane & 15);
         if (p >= pe) continue;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          double sm = (double)(acc[c][0][r] + cr[r][0]);  // exact: |Σ| < 2^53 for N < 2^18
-#pragma unroll
-          for (int d = 1; d < Q8_DIGITS; ++d) sm = fma(sm, 128.0, (double)(acc[c][d][r] + cr[r][d]));
-          v[r] = (float)(sm * sc[r]);
-        }
+        for (int r = 0; r < 4; ++r) v[r] = value(c, r);
         q8_store<K, LAYOUT>(dst, P, p, g, v);
       }
     }
@@ -185,18 +214,18 @@ fit_q8(const unsigned char* __restrict__ op, int N, const unsigned char* __restr
   __syncthreads();
   const int S2 = S + (S & 1);
   for (int s = 0; s < S2; s += 2) {
-    if (s > 0 && s % T == 0) finish(s / T - 1);
+    if (s > 0 && s % T == 0) finish(s / T - 1, 1);
     load(min(s + 2, S - 1), sa);
     compute(0, s % T);
     park(1, sb);
     __syncthreads();
-    if (s + 1 < S && (s + 1) % T == 0) finish((s + 1) / T - 1);
+    if (s + 1 < S && (s + 1) % T == 0) finish((s + 1) / T - 1, 0);
     load(min(s + 3, S - 1), sb);
     if (s + 1 < S) compute(1, (s + 1) % T);
     park(0, sa);
     __syncthreads();
   }
-  finish(ntiles - 1);
+  finish(ntiles - 1, 0);
 }
 
 struct Q8Args {
@@ -211,6 +240,7 @@ struct Q8Args {
   hipStream_t s;
   int64_t pb = 0, pe = 0;
   int tpw = 1;  // consecutive tiles streamed by one workgroup
+  bool stage = false;  // pixel-major rows staged through LDS (RTI_KERNEL_STAGE)
 };
 
 size_t q8_lds_bytes(int N) { return (size_t)q8_operator_bytes(N) + (size_t)2 * Q8_STEP * Q8_RS; }
@@ -218,7 +248,7 @@ size_t q8_lds_bytes(int N) { return (size_t)q8_operator_bytes(N) + (size_t)2 * Q
 template <int K, int LAYOUT>
 int launch_q8_t(const Q8Args& a) {
   const size_t lds = q8_lds_bytes(a.N);
-  auto kern = fit_q8<K, LAYOUT>;
+  auto kern = a.stage ? fit_q8<K, LAYOUT, true> : fit_q8<K, LAYOUT, false>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_q8: cannot reserve %zu B of LDS", lds);
@@ -295,6 +325,7 @@ extern "C" int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I,
   // channel, each streamed by the same workgroups (the fp32 stream's launch generations, rti_fit.hip)
   const int64_t tpc = (P + Q8_R - 1) / Q8_R, cus = device_cus();
   const int want = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  a.stage = (kernel & RTI_KERNEL_STAGE) != 0;
   const int parts = std::max(1, (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF);
   const int64_t wpc = cus >= C ? cus / C : 1;  // workgroups per channel: at most one per CU over all channels
   const int64_t tpp = (tpc + parts - 1) / parts;  // tiles per part

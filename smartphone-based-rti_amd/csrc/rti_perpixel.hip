@@ -400,12 +400,12 @@ __device__ __forceinline__ void ne_sub(Normal6& ne, float lu, float lv, double L
   ne.b[5] -= L;
 }
 
-// VAR (measurement switch RTI_PERPIXEL_VARIANT, default 2): 0 = two Newton steps, an ambiguous pixel marked
+// VAR (measurement switch RTI_PERPIXEL_VARIANT, default 3): 0 = two Newton steps, an ambiguous pixel marked
 // for the refine pass; 1 = one step, marked; 2 = one step, fixed up in place per group of 4 lights;
-// 3 = 2 at 5 waves per SIMD (96 VGPRs: the fix-up's IEEE temporaries without spills).
+// 3 = 2 at 5 waves per SIMD (96 VGPRs: the fix-up's IEEE temporaries without spills); 4 = 2 at 4 waves.
 template <typename T, typename TC, int LAYOUT, int VAR>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(VAR == 3 ? 5 : 6)))
+__attribute__((amdgpu_waves_per_eu(VAR == 3 ? 5 : (VAR == 4 ? 4 : 6))))
 fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
                  double x0, double y0, double rcond, TC* __restrict__ coef) {
   constexpr int NW = VAR == 0 ? 2 : 1;
@@ -622,10 +622,11 @@ void launch_cam(const double* cams, int N, const void* I, int H, int W, int64_t 
                 double rcond, void* coef, hipStream_t s) {
   const int64_t P = (int64_t)H * W;
   const char* ev = getenv("RTI_PERPIXEL_VARIANT");  // measurement switch, read per call (A/B in one process)
-  const int var = ev ? atoi(ev) : 2;
+  const int var = ev ? atoi(ev) : 3;
   auto kern = var == 0 ? fit_perpixel_cam<T, TC, LAYOUT, 0>
              : var == 1 ? fit_perpixel_cam<T, TC, LAYOUT, 1>
-             : var == 3 ? fit_perpixel_cam<T, TC, LAYOUT, 3> : fit_perpixel_cam<T, TC, LAYOUT, 2>;
+             : var == 2 ? fit_perpixel_cam<T, TC, LAYOUT, 2>
+             : var == 4 ? fit_perpixel_cam<T, TC, LAYOUT, 4> : fit_perpixel_cam<T, TC, LAYOUT, 3>;
   hipLaunchKernelGGL(kern, dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N, static_cast<const T*>(I), H, W, ls, x0,
                      y0, rcond, static_cast<TC*>(coef));
   hipLaunchKernelGGL((refine_cam<T, TC, LAYOUT>), refine_grid(P), dim3(256), 0, s, cams, N,
