@@ -276,12 +276,15 @@ int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp,
  * for every pixel: nodes x_n = (lu[p][n], lv[p][n]) and values I[p][n], PIXEL-major as
  * compute_intensities returns them; A_ij = ‖x_i − x_j‖, A w = I solved to fp64 accuracy (what
  * SciPy's LU with partial pivoting returns, to rounding: fp64 Gauss-Jordan for N <= 80, an fp32
- * Gauss-Jordan inverse + fp64 iterative refinement above), f(q_e) = Σ_n w_n ‖q_e − x_n‖
+ * Gauss-Jordan inverse + fp64 iterative refinement to 256 with an fp64 partial-pivoting fallback
+ * for ill-conditioned pixels, a blocked fp64 Cholesky of the bordered system above 256),
+ * f(q_e) = Σ_n w_n ‖q_e − x_n‖
  * evaluated in fp64 at luv[E][2] (device).
  * out: F64 / F32 / I32 / U8, layout RTI_OUT_PIXEL_MAJOR ([p][e], the reference's
  * [y][x][ly][lx]) or RTI_OUT_EVAL_MAJOR ([e][p], prepare_images_data's [ly][lx][y][x]).
  * status: device int the caller zeroes; set to RTI_ERR_SINGULAR when a pixel's system is
- * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 256. */
+ * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 2556
+ * (RTI_ERR_UNSUPPORTED above: the Cholesky panel's LDS). */
 int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                      const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
                      rti_stream_t stream);

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 
 #include "rti_convert.h"
@@ -355,7 +356,8 @@ int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int 
   const size_t lds = (size_t)(EXACT ? 1 : 2) * TP16 * (Kp + 8) * sizeof(_Float16);
   const unsigned gx = (unsigned)((P + TP16 - 1) / TP16);
   const int nwb = (E + 127) / 128;  // 4 waves × 32-row blocks per sweep step
-  const unsigned gy = (unsigned)std::max(1, std::min(nwb, (int)((2048 + gx - 1) / gx)));
+  unsigned gy = (unsigned)std::max(1, std::min(nwb, (int)((2048 + gx - 1) / gx)));
+  if (const char* e = getenv("RTI_OP_GY")) gy = (unsigned)std::max(1, std::min(nwb, atoi(e)));  // measurement
   dim3 grid(gx, gy, C);
   if (lds > 65536) {
     auto k = vec ? apply_op_f16s<T, TO, true> : apply_op_f16s<T, TO, false>;
