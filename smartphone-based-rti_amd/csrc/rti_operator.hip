@@ -356,7 +356,12 @@ int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int 
   const size_t lds = (size_t)(EXACT ? 1 : 2) * TP16 * (Kp + 8) * sizeof(_Float16);
   const unsigned gx = (unsigned)((P + TP16 - 1) / TP16);
   const int nwb = (E + 127) / 128;  // 4 waves × 32-row blocks per sweep step
-  unsigned gy = (unsigned)std::max(1, std::min(nwb, (int)((2048 + gx - 1) / gx)));
+  // E-split: one sweep over all row blocks per pixel tile once the tiles alone give two workgroups per CU
+  // (c7 400²×100 → 10⁴ tables, 1250 tiles: 1.302 ms against 1.424 ms split in 2 and 1.549 in 3,
+  // profiles/r03_c7_gy_sweep.log — each split re-stages the tile and halves the rows its prologue pays for);
+  // smaller images split the rows until the grid reaches that
+  const int want = 2 * device_cus();
+  unsigned gy = (unsigned)std::max(1, std::min(nwb, (int)((want + gx - 1) / gx)));
   if (const char* e = getenv("RTI_OP_GY")) gy = (unsigned)std::max(1, std::min(nwb, atoi(e)));  // measurement
   dim3 grid(gx, gy, C);
   if (lds > 65536) {
