@@ -402,10 +402,11 @@ __device__ __forceinline__ void ne_sub(Normal6& ne, float lu, float lv, double L
 
 // VAR (measurement switch RTI_PERPIXEL_VARIANT, default 3): 0 = two Newton steps, an ambiguous pixel marked
 // for the refine pass; 1 = one step, marked; 2 = one step, fixed up in place per group of 4 lights;
-// 3 = 2 at 5 waves per SIMD (96 VGPRs: the fix-up's IEEE temporaries without spills); 4 = 2 at 4 waves.
+// 3 = 2 at 5 waves per SIMD (96 VGPRs: the fix-up's IEEE temporaries without spills); 4 = 2 at 4 waves;
+// 5 = 3 with every group fixed up (test-only: exercises the replace path on any input).
 template <typename T, typename TC, int LAYOUT, int VAR>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(VAR == 3 ? 5 : (VAR == 4 ? 4 : 6))))
+__attribute__((amdgpu_waves_per_eu(VAR == 3 || VAR == 5 ? 5 : (VAR == 4 ? 4 : 6))))
 fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I, int H, int W, int64_t lstride,
                  double x0, double y0, double rcond, TC* __restrict__ coef) {
   constexpr int NW = VAR == 0 ? 2 : 1;
@@ -454,12 +455,12 @@ fit_perpixel_cam(const double* __restrict__ cams, int N, const T* __restrict__ I
       DirCheck<NW> chk;
 #pragma unroll
       for (int u = 0; u < 4; ++u) light(n + u, chk);
-      if (__builtin_expect(chk.ambiguous(), 0)) fix(n, 4);
+      if (__builtin_expect(VAR == 5 || chk.ambiguous(), 0)) fix(n, 4);
     }
     for (; n < N; ++n) {
       DirCheck<NW> chk;
       light(n, chk);
-      if (__builtin_expect(chk.ambiguous(), 0)) fix(n, 1);
+      if (__builtin_expect(VAR == 5 || chk.ambiguous(), 0)) fix(n, 1);
     }
     ne_finish(ne, N);
     solve_store<TC, LAYOUT>(ne, rcond, coef, P, p);
@@ -626,7 +627,8 @@ void launch_cam(const double* cams, int N, const void* I, int H, int W, int64_t 
   auto kern = var == 0 ? fit_perpixel_cam<T, TC, LAYOUT, 0>
              : var == 1 ? fit_perpixel_cam<T, TC, LAYOUT, 1>
              : var == 2 ? fit_perpixel_cam<T, TC, LAYOUT, 2>
-             : var == 4 ? fit_perpixel_cam<T, TC, LAYOUT, 4> : fit_perpixel_cam<T, TC, LAYOUT, 3>;
+             : var == 4 ? fit_perpixel_cam<T, TC, LAYOUT, 4>
+             : var == 5 ? fit_perpixel_cam<T, TC, LAYOUT, 5> : fit_perpixel_cam<T, TC, LAYOUT, 3>;
   hipLaunchKernelGGL(kern, dim3(grid_1d(P, 256)), dim3(256), 0, s, cams, N, static_cast<const T*>(I), H, W, ls, x0,
                      y0, rcond, static_cast<TC*>(coef));
   hipLaunchKernelGGL((refine_cam<T, TC, LAYOUT>), refine_grid(P), dim3(256), 0, s, cams, N,

@@ -185,3 +185,29 @@ def test_perpixel_all_pixels_ill_conditioned(cuda):
     err, ok = coef_close(coef, np.broadcast_to(ref, coef.shape), rtol=1e-6)
     report("perpixel dirs, all refined", "nearcollinear", err)
     assert ok, err
+
+
+@pytest.mark.parametrize("var", ["0", "1", "2", "3", "4", "5"])
+def test_perpixel_cam_variants(cuda, monkeypatch, var):
+    """Every exactness variant of the fused per-pixel fit (RTI_PERPIXEL_VARIANT, rti_perpixel.hip: two or one
+    Newton steps with the refine pass, the in-place group fix-up at 6 / 5 / 4 waves per SIMD, and 5 = every
+    group fixed up, which drives the subtract-and-replace path on any input) against the fp64 SVD of each
+    pixel's own design with the reference's light vectors, on a 48 × 40 ROI plus the near-collinear golden
+    pixel (the QR refine)."""
+    monkeypatch.setenv("RTI_PERPIXEL_VARIANT", var)
+    for case, (H, W) in (("n200", (48, 40)), ("nearcollinear", (5, 7))):
+        lu0, lv0, I, _ = edge(case)
+        cams = cams_for(lu0, lv0, 2.0, 1.0, 40.0)
+        N = cams.shape[0]
+        rng = np.random.default_rng(11)
+        Ist = (I[:, None, None] + rng.integers(-3, 4, size=(N, H, W))).astype(np.float32)
+        coef = rti.fit(torch.as_tensor(Ist, device=cuda), mode="perpixel", cams=cams,
+                       coef_dtype=torch.float64).cpu().numpy().reshape(-1, 6)
+        ys, xs = np.mgrid[0:H, 0:W]
+        px = np.unique(np.r_[np.random.default_rng(3).integers(0, H * W, 64), 0, H * W - 1, 1 * W + 2])
+        lu, lv = o.light_dirs_for_pixels(cams, xs.ravel()[px], ys.ravel()[px])
+        refs = np.stack([o.svd_solve(design_xx(lu[i], lv[i]), Ist.reshape(N, -1)[:, p].astype(np.float64))
+                         for i, p in enumerate(px)])
+        err, ok = coef_close(coef[px], refs, rtol=1e-6)
+        report(f"perpixel cam variant {var}", case, err)
+        assert ok, (case, err)
