@@ -167,7 +167,7 @@ def synth_cams(n, seed, H, W):
 # is reported only while these files are byte-identical to the ones the counters were taken on
 KERNEL_SOURCES = {
     "fit_shared_valu": ["rti_fit.hip"], "fit_shared_tile": ["rti_fit.hip"], "fit_shared_mfma": ["rti_fit.hip"],
-    "fit_q8": ["rti_fit_q8.hip", "rti_q8.h"], "fit_shared_residual_k": ["rti_fitres.hip"],
+    "fit_q8": ["rti_fit_q8.hip", "rti_q8.h"], "fit_h16": ["rti_fit_h16.hip"], "fit_shared_residual_k": ["rti_fitres.hip"],
     "fit_residual_k": ["rti_residual.hip"], "relight_eval": ["rti_relight.hip", "rti_convert.h"],
     "relight_frame": ["rti_relight.hip", "rti_convert.h"], "fit_perpixel_cam": ["rti_perpixel.hip"],
     "apply_op": ["rti_operator.hip"], "rbf_": ["rti_rbf.hip"],
@@ -314,10 +314,18 @@ class FitWorkload(Workload):
         self.dtype = "f32" if args.in_dtype == "f32" else f"{args.in_dtype} in / f32 compute"
         L = rti._lib
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        self.q8 = args.kernel in ("auto", "q8") and rti.api.q8_supported(self.I, k, N, P)
-        if self.q8:  # 8-bit stacks: rti.fit's AUTO path, the int8-MFMA fixed-point fit (rti_fit_q8.hip)
-            self.op_dev = torch.as_tensor(rti.q8_operator(self.pinv64), device=dev)
-            fn, fname = L.lib().rti_fit_shared_q8, "rti_fit_shared_q8"
+        # 8-bit stacks: rti.fit's AUTO path, the split-fp16 fit on the fp16 matrix cores (rti_fit_h16.hip), or
+        # with --kernel q8 the int8 fixed-point form (rti_fit_q8.hip)
+        mk = "h16" if args.kernel == "auto" else args.kernel
+        self.q8 = mk in ("h16", "q8") and rti.api.q8_supported(self.I, k, N, P, mk)
+        self.u8_kernel = mk if self.q8 else None
+        if self.q8:
+            if mk == "h16":
+                self.op_dev = torch.as_tensor(rti.h16_operator(self.pinv64), device=dev)
+                fn, fname = L.lib().rti_fit_shared_h16, "rti_fit_shared_h16"
+            else:
+                self.op_dev = torch.as_tensor(rti.q8_operator(self.pinv64), device=dev)
+                fn, fname = L.lib().rti_fit_shared_q8, "rti_fit_shared_q8"
             cargs = (ctypes.c_void_p(self.op_dev.data_ptr()), k, N, ctypes.c_void_p(self.I.data_ptr()), P, C, P, N * P,
                      ctypes.c_void_p(self.coef.data_ptr()), rti.api._layout_id(args.layout), P * k, 0, stream)
         else:
@@ -335,8 +343,10 @@ class FitWorkload(Workload):
         self.step = step
         step(0)
         self.launches = int(L.lib().rti_last_launch_count())
-        if self.q8:
+        if self.u8_kernel == "q8":
             self.dtype = "u8 in / int8 MFMA on a 4-digit 27-bit fixed-point operator, exact int32 sums / f32 out"
+        elif self.u8_kernel == "h16":
+            self.dtype = "u8 in / fp16 MFMA on a split-fp16 (22-bit) operator, fp32 sums / f32 out"
 
     def traffic(self):
         if self.ctx.world != 1 or self.ctx.weak:
@@ -347,7 +357,7 @@ class FitWorkload(Workload):
 
     def config(self):
         return {"lights": self.N, "channels": self.C, "basis": self.basis, "k": self.k,
-                "coef_layout": self.args.layout, "kernel": "q8" if self.q8 else self.args.kernel,
+                "coef_layout": self.args.layout, "kernel": self.u8_kernel or self.args.kernel,
                 "intensity_dtype": self.args.in_dtype}
 
     def coef_pk(self, c):
@@ -1011,7 +1021,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--weak", action="store_true", help="every rank fits a whole H-row image (weak scaling)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma", "tile", "q8"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma", "tile", "q8", "h16"])
     ap.add_argument("--layout", default="pixel", choices=["pixel", "planar"])
     ap.add_argument("--nontemporal", action="store_true")
     ap.add_argument("--in-dtype", default="f32", choices=["f32", "u8", "i32"],

@@ -160,6 +160,21 @@ int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I, int64_t P,
                       float* coef, int coef_layout, int64_t coef_channel_stride,
                       int kernel, rti_stream_t stream);
 
+/* ---- device: shared fit of 8-bit stacks on the fp16 matrix cores (rti_fit_h16.hip) ----
+ * The same contraction as rti_fit_shared_q8 with the operator split as w·s = hi + lo in fp16 (s a power
+ * of two per row: 22 significant bits) and fp32 accumulation (v_mfma_f32_16x16x32_f16): the accuracy of
+ * the fp32 stream, a quarter of the q8 form's accumulator registers per pixel, so 2048-pixel tiles and
+ * 2-KiB runs per wave and plane.  rti_h16_operator builds the operator (rti_h16_operator_bytes(k, N)
+ * bytes, device copy 16-byte aligned) from the fp64 pseudo-inverse (non-finite entries -> RTI_ERR_BAD_ARG).
+ * Arguments, alignment and layouts as rti_fit_shared_q8; N <= rti_fit_shared_h16_max_lights(). */
+int64_t rti_h16_operator_bytes(int k, int N);
+int rti_h16_operator(const double* pinv, int k, int N, void* op);
+int rti_fit_shared_h16_max_lights(void);
+int rti_fit_shared_h16(const void* op, int k, int N, const uint8_t* I, int64_t P, int C,
+                       int64_t light_stride, int64_t channel_stride,
+                       float* coef, int coef_layout, int64_t coef_channel_stride,
+                       int kernel, rti_stream_t stream);
+
 /* ---- device: per-pixel residuals of the shared-direction fit -----------------------
  * Fit quality next to rti_fit_shared's coefficients (the reference computes the same
  * least-squares solution, analysis.py:280-298, and never reports its residual):

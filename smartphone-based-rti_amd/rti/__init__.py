@@ -12,13 +12,13 @@ from . import _lib
 from ._lib import RTIError, RTILibraryMissing
 from .api import (BASES, apply_operator, basis_eval, basis_id, basis_operator, basis_terms, design_matrix, fit,
                   fit_residual, fit_shared_into, fit_shared_residual_into, fit_with_residual, gram_inverse,
-                  interpolate_rbf, interpolate_rbf_perpixel, light_dirs, lsq_factors, pinv, q8_operator, rbf_operator,
+                  interpolate_rbf, interpolate_rbf_perpixel, light_dirs, lsq_factors, pinv, q8_operator, h16_operator, rbf_operator,
                   relight, relight_frame)
 
 __all__ = ["BASES", "RTIError", "RTILibraryMissing", "apply_operator", "basis_eval", "basis_id", "basis_operator",
            "basis_terms", "design_matrix", "fit", "fit_residual", "fit_shared_into", "fit_shared_residual_into",
            "fit_with_residual", "gram_inverse", "interpolate_rbf", "interpolate_rbf_perpixel", "light_dirs",
-           "lsq_factors", "pinv", "q8_operator",
+           "lsq_factors", "pinv", "q8_operator", "h16_operator",
            "rbf_operator", "relight", "relight_frame", "library_path", "load"]
 
 __version__ = "0.1.0"

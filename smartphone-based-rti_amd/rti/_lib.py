@@ -89,6 +89,11 @@ SIGNATURES = {
     "rti_fit_shared_q8_max_lights": (_c_int, []),
     "rti_fit_shared_q8": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_i64, _c_int, _c_i64, _c_i64, _c_void_p,
                                    _c_int, _c_i64, _c_int, _c_void_p]),
+    "rti_h16_operator_bytes": (_c_i64, [_c_int, _c_int]),
+    "rti_h16_operator": (_c_int, [_c_double_p, _c_int, _c_int, _c_void_p]),
+    "rti_fit_shared_h16_max_lights": (_c_int, []),
+    "rti_fit_shared_h16": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_i64, _c_int, _c_i64, _c_i64, _c_void_p,
+                                    _c_int, _c_i64, _c_int, _c_void_p]),
     "rti_fit_residual_blocks": (_c_i64, [_c_i64]),
     "rti_fit_residual": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_int, _c_i64, _c_int, _c_i64, _c_i64,
                                   _c_void_p, _c_int, _c_i64, _c_void_p, _c_void_p, _c_void_p]),

@@ -129,10 +129,37 @@ def q8_operator(pinv64):
     return op
 
 
-def q8_supported(I, k, N, P):
-    """Whether ``rti_fit_shared_q8`` takes this contiguous stack of P-pixel planes (uint8, k in {6, 9, 16}, N
-    within its LDS budget, 16-byte aligned planes)."""
-    if I.dtype != torch.uint8 or k not in (6, 9, 16) or N > int(L.lib().rti_fit_shared_q8_max_lights()):
+def h16_operator(pinv64):
+    """Host: the split-fp16 form of an fp64 operator [k, N] for ``rti_fit_shared_h16`` (8-bit stacks on the
+    fp16 matrix cores; layout in csrc/rti_fit_h16.hip).  Raises ValueError for non-finite entries."""
+    pv = np.ascontiguousarray(np.asarray(pinv64, np.float64))
+    k, N = pv.shape
+    nb = int(L.lib().rti_h16_operator_bytes(k, N))
+    if nb <= 0:
+        raise ValueError(f"no h16 operator for k={k}, N={N}")
+    op = np.zeros(nb, dtype=np.uint8)
+    L.check(L.lib().rti_h16_operator(_dptr(pv), k, N, ctypes.c_void_p(op.ctypes.data)), "rti_h16_operator")
+    return op
+
+
+def fit_h16_into(op_dev, I, coef, *, k, layout="pixel", flags=0):
+    """Launch ``rti_fit_shared_h16`` on preallocated tensors: op_dev = h16_operator(...) on the device
+    (uint8), I a contiguous uint8 CUDA [N, P] or [C, N, P] stack, coef fp32 as fit_shared_into."""
+    if I.dim() == 2:
+        C, (N, P) = 1, I.shape
+    else:
+        C, N, P = I.shape
+    st = L.lib().rti_fit_shared_h16(_vp(op_dev), k, N, _vp(I), P, C, P, N * P, _vp(coef), _layout_id(layout),
+                                    P * k, int(flags), _stream_of(I))
+    L.check(st, "rti_fit_shared_h16")
+    return coef
+
+
+def q8_supported(I, k, N, P, kernel="q8"):
+    """Whether ``rti_fit_shared_q8`` (kernel="q8") or ``rti_fit_shared_h16`` (kernel="h16") takes this contiguous
+    stack of P-pixel planes (uint8, k in {6, 9, 16}, N within the kernel's LDS budget, 16-byte aligned planes)."""
+    fn = L.lib().rti_fit_shared_h16_max_lights if kernel == "h16" else L.lib().rti_fit_shared_q8_max_lights
+    if I.dtype != torch.uint8 or k not in (6, 9, 16) or N > int(fn()):
         return False
     return P % 16 == 0 and I.data_ptr() % 16 == 0
 
@@ -242,15 +269,19 @@ def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=Non
         Ic = I.contiguous().reshape(C, N, P)
         shape = (C, P, k) if cl == L.RTI_COEF_PIXEL_MAJOR else (C, k, P)
         coef = torch.empty(shape, dtype=torch.float32, device=I.device)
-        # 8-bit stacks (the reference's V channel): the int8-MFMA fixed-point fit when the operator is finite
-        # (a rank-deficient light set without rcond keeps the fp32 path and the reference's NaN)
-        if kernel in ("auto", "q8") and q8_supported(Ic, k, N, P) and np.isfinite(pv).all():
-            op_dev = torch.as_tensor(q8_operator(pv), device=I.device)
-            fit_q8_into(op_dev, Ic, coef, k=k, layout=cl)
-        elif kernel == "q8":
-            raise NotImplementedError("kernel='q8' needs a uint8 stack, k in (6, 9, 16), N <= "
-                                      f"{int(L.lib().rti_fit_shared_q8_max_lights())}, 16-pixel-aligned planes and a "
-                                      "finite pseudo-inverse")
+        # 8-bit stacks (the reference's V channel): AUTO runs the split-fp16 fit on the fp16 matrix cores
+        # (kernel="h16"); kernel="q8" the int8 fixed-point form (exact sums); both need a finite
+        # operator (a rank-deficient light set without rcond keeps the fp32 path and the reference's NaN)
+        mk = "h16" if kernel == "auto" else kernel
+        if mk in ("h16", "q8") and q8_supported(Ic, k, N, P, mk) and np.isfinite(pv).all():
+            if mk == "h16":
+                fit_h16_into(torch.as_tensor(h16_operator(pv), device=I.device), Ic, coef, k=k, layout=cl)
+            else:
+                fit_q8_into(torch.as_tensor(q8_operator(pv), device=I.device), Ic, coef, k=k, layout=cl)
+        elif kernel in ("q8", "h16"):
+            fn = L.lib().rti_fit_shared_h16_max_lights if kernel == "h16" else L.lib().rti_fit_shared_q8_max_lights
+            raise NotImplementedError(f"kernel={kernel!r} needs a uint8 stack, k in (6, 9, 16), N <= {int(fn())}, "
+                                      "16-pixel-aligned planes and a finite pseudo-inverse")
         else:
             pinv_dev = torch.as_tensor(pv.astype(np.float32), device=I.device)
             fit_shared_into(pinv_dev, Ic, coef, k=k, layout=cl, kernel=kernel, nontemporal=nontemporal)

@@ -196,3 +196,37 @@ def test_q8_operator_rejects_non_finite():
     e = golden("ptm_edge.npz")
     with pytest.raises(ValueError, match="non-finite"):
         rti.q8_operator(rti.pinv(e["singular_lu"], e["singular_lv"]))
+
+
+@pytest.mark.parametrize("basis,N", [("ptm", 20), ("ptm", 100), ("hsh", 200), ("hsh9", 33)])
+def test_h16_operator_split_fp16(basis, N):
+    """rti_h16_operator (host): per coefficient row a power-of-two scale s with max|w·s| in [2^14, 2^15), the
+    weights split as w·s = hi + lo in fp16 (22 significant bits: |hi + lo − w·s| <= 2^-22·max|w·s|), rows
+    >= k and lights >= N zero, inv_s = 1/s; and the product the kernel forms (exact fp16 intensities, fp32-like
+    sums) reproduces pinv·I."""
+    lu, lv = o.synth_dirs(N, 9)
+    pv = rti.pinv(lu, lv, basis)
+    k = pv.shape[0]
+    op = rti.h16_operator(pv)
+    assert op.size == rti._lib.lib().rti_h16_operator_bytes(k, N)
+    Np = (N + 31) // 32 * 32
+    hi = op[:16 * Np * 2].view(np.float16).reshape(16, Np).astype(np.float64)
+    lo = op[16 * Np * 2:32 * Np * 2].view(np.float16).reshape(16, Np).astype(np.float64)
+    inv_s = op[32 * Np * 2:].view(np.float32).astype(np.float64)
+    assert not hi[k:].any() and not lo[k:].any() and not hi[:, N:].any() and not lo[:, N:].any()
+    s = 1.0 / inv_s[:k]
+    assert np.array_equal(np.log2(s), np.round(np.log2(s)))  # powers of two
+    ws = pv * s[:, None]
+    mx = np.abs(ws).max(1)
+    assert (mx >= 2.0 ** 14).all() and (mx < 2.0 ** 15).all()
+    assert (np.abs(hi[:k, :N] + lo[:k, :N] - ws) <= 2.0 ** -22 * mx[:, None]).all()
+    I = np.random.default_rng(N).integers(0, 256, (N, 555)).astype(np.float64)
+    c = ((hi[:k, :N] + lo[:k, :N]) @ I) * inv_s[:k, None]
+    ref = pv @ I
+    assert (np.abs(c - ref) <= 2.0 ** -21 * np.abs(pv).max(1)[:, None] * I.sum(0)[None, :]).all()
+
+
+def test_h16_operator_rejects_non_finite():
+    e = golden("ptm_edge.npz")
+    with pytest.raises(ValueError, match="non-finite"):
+        rti.h16_operator(rti.pinv(e["singular_lu"], e["singular_lv"]))

@@ -1,5 +1,5 @@
-"""GPU parity of the 8-bit fit on the int8 matrix cores (rti_fit_shared_q8, AUTO for uint8 stacks in
-rti.fit): the reference's golden coefficients, the fp64 oracle over every supported basis, light counts
+"""GPU parity of the 8-bit fit on the int8 matrix cores (rti_fit_shared_q8, rti.fit(kernel="q8"); AUTO for
+uint8 stacks is the split-fp16 form, tests/test_gpu_h16.py): the reference's golden coefficients, the fp64 oracle over every supported basis, light counts
 around the 64-light steps and the LDS limit, ragged pixel counts (partial tiles), two channels, both
 layouts, launch generations, and the fallbacks (fp32 path) where q8 does not apply.
 
@@ -37,7 +37,7 @@ def test_golden_256x256_N20(cuda):
     d = golden("ptm_shared_256x256_N20.npz")
     I = np.asarray(d["I"]).astype(np.uint8)
     assert np.array_equal(I, d["I"])  # the golden stack is integer 0..255
-    coef = fit_u8(I, d["lu"], d["lv"], "ptm", cuda).cpu().numpy()
+    coef = fit_u8(I, d["lu"], d["lv"], "ptm", cuda, kernel="q8").cpu().numpy()
     err, ok = coef_close(coef, d["coef"], rtol=1e-6)  # the reference's own coefficients (analysis.py:293-298)
     print(f"q8 vs reference golden: {err:.3g}")
     assert ok, err
@@ -54,7 +54,8 @@ def test_vs_oracle(cuda, basis, N, layout):
     rng = np.random.default_rng(N * 31 + k)
     for P in (16, 1024, 1040, 3 * 1024 + 16 * 7):
         I = rng.integers(0, 256, size=(2, N, P), dtype=np.uint8)
-        coef = rti.fit(torch.as_tensor(I, device=cuda)[..., None], lu, lv, basis=basis, layout=layout).cpu().numpy()
+        coef = rti.fit(torch.as_tensor(I, device=cuda)[..., None], lu, lv, basis=basis, layout=layout,
+                       kernel="q8").cpu().numpy()
         pv = np.linalg.pinv(o.design("ptm" if basis == "ptm" else "hsh", lu, lv)[:, :k])
         for c in range(2):
             got = coef[c].reshape(P, k) if layout == "pixel" else coef[c].reshape(k, P).T
@@ -70,7 +71,7 @@ def test_max_lights_and_extremes(cuda):
     for fill in (0, 255, None):
         I = (np.full((Nmax, 2048), fill, np.uint8) if fill is not None
              else np.random.default_rng(2).integers(0, 256, (Nmax, 2048), dtype=np.uint8))
-        coef = rti.fit(torch.as_tensor(I, device=cuda), lu, lv, basis="hsh").cpu().numpy()
+        coef = rti.fit(torch.as_tensor(I, device=cuda), lu, lv, basis="hsh", kernel="q8").cpu().numpy()
         ref = (pv @ I.astype(np.float64)).T
         if fill == 0:
             assert not coef.any()
@@ -80,8 +81,8 @@ def test_max_lights_and_extremes(cuda):
 
 
 def test_q8_matches_fp32_stream_and_is_used(cuda):
-    """AUTO on uint8 runs rti_fit_shared_q8 (its launch count is the q8 generations'), and agrees with the fp32
-    stream on the same stack within the fp32 stream's own rounding."""
+    """kernel="q8" on uint8 runs rti_fit_shared_q8 and agrees with the fp32 stream on the same stack within the
+    fp32 stream's own rounding, and is closer to fp64 than it."""
     lu, lv = o.synth_dirs(100, 2)
     I = torch.as_tensor(o.synth_intensities(216, 384, lu, lv, seed=3), device=cuda).round().clamp(0, 255)
     a = rti.fit(I.to(torch.uint8), lu, lv, kernel="q8")

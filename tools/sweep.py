@@ -47,6 +47,8 @@ def main():
         I = I.to(torch.uint8 if args.in_dtype == "u8" else torch.int32)
     pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=dev)
     op_dev = torch.as_tensor(rti.q8_operator(rti.pinv(lu, lv, basis)), device=dev) if args.in_dtype == "u8" else None
+    h16_dev = torch.as_tensor(rti.api.h16_operator(rti.pinv(lu, lv, basis)), device=dev) \
+        if args.in_dtype == "u8" else None
     coefs = {"pixel": torch.empty((C, P, k), device=dev), "planar": torch.empty((C, k, P), device=dev)}
     variants = []
     for v in args.variants.split(","):
@@ -121,6 +123,8 @@ def main():
         elif kern == "pfit":
             probe.probe_fit6(ctypes.c_void_p(pv.data_ptr()), ctypes.c_void_p(I.data_ptr()), N, P,
                              ctypes.c_void_p(coefs["pixel"].data_ptr()), int(layout), ctypes.c_void_p(stream.cuda_stream))
+        elif kern == "h16":
+            rti.api.fit_h16_into(h16_dev, I, coefs[layout], k=k, layout=layout, flags=fl)
         elif kern == "q8":
             rti.api.fit_q8_into(op_dev, I, coefs[layout], k=k, layout=layout, flags=fl)
         else:
@@ -131,7 +135,7 @@ def main():
     for name, kern, layout, fl in variants:  # warm-up
         for _ in range(3):
             launch(kern, layout, fl)
-        if kern in ("valu", "mfma", "tile", "auto", "q8"):
+        if kern in ("valu", "mfma", "tile", "auto", "q8", "h16"):
             got = coefs[layout] if layout == "pixel" else coefs[layout].transpose(1, 2)
             got = got.double()
             if ref is None:
