@@ -18,8 +18,10 @@ for k in ${KEYS:-c3 c2 c4 c3u8 c4u8 c10 c6 c7 c5 c9}; do
     c3) run c3-auto-pixel "--config c3" fit_shared_valu 3516825600 4;;
     c2) run c2-auto-pixel "--config c2" fit_shared_valu 464486400 1;;
     c4) run c4-auto-pixel "--config c4" fit_shared_tile_w 21499084800 6;;
-    c3u8) run c3-auto-pixel-u8 "--config c3 --in-dtype u8" fit_q8 1028505600 1;;
-    c4u8) run c4-auto-pixel-u8 "--config c4 --in-dtype u8" fit_q8 6569164800 1;;
+    c3u8) run c3-auto-pixel-u8 "--config c3 --in-dtype u8" fit_h16 1028505600 1;;
+    c4u8) run c4-auto-pixel-u8 "--config c4 --in-dtype u8" fit_h16 6569164800 1;;
+    c3q8) run c3-q8-pixel-u8 "--config c3 --in-dtype u8 --kernel q8" fit_q8 1028505600 1;;
+    c4q8) run c4-q8-pixel-u8 "--config c4 --in-dtype u8 --kernel q8" fit_q8 6569164800 1;;
     c10) run c10 "--config c10" fit_shared_residual_k 3550003200 8;;
     c6) run c6 "--config c6" fit_perpixel_cam 3516825600 1;;
     c7) run c7-split16 "--config c7" apply_op 6464000000 1;;
