@@ -192,10 +192,11 @@ def sources_sha16(files):
     return h.hexdigest()[:16]
 
 
-def load_traffic(workload_key):
+def load_traffic(workload_key, family=None):
     """PMC bytes per step for this workload from profiles/traffic.json, with its provenance: reported only when
     the kernel source files the counters were taken on (entry['sources'], hashed as entry['src_sha16']) are
-    unchanged — a kernel edited since its PMC pass yields traffic None and traffic_source.stale = true."""
+    unchanged and, when the caller names the kernel family it launched (e.g. "fit_h16"), the profiled kernel
+    symbol is of that family — otherwise traffic None and traffic_source.stale = true."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
@@ -211,7 +212,8 @@ def load_traffic(workload_key):
         now = sources_sha16(files) if files else None
     except OSError:
         now = None
-    src["stale"] = not (files and now == entry.get("src_sha16"))
+    src["stale"] = not (files and now == entry.get("src_sha16")) or \
+        bool(family and family not in (entry.get("kernel_symbol") or ""))
     if src["stale"]:
         return None, src
     # per step: launch generations split one step into launches_per_step launches
@@ -353,7 +355,7 @@ class FitWorkload(Workload):
             return None  # the PMC figures in profiles/traffic.json are for the whole image
         a = self.args
         key = f"{a.config}-{a.kernel}-{a.layout}" + ("" if a.in_dtype == "f32" else f"-{a.in_dtype}")
-        return load_traffic(key)
+        return load_traffic(key, f"fit_{self.u8_kernel}" if self.u8_kernel else None)
 
     def config(self):
         return {"lights": self.N, "channels": self.C, "basis": self.basis, "k": self.k,
