@@ -905,15 +905,22 @@ rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const
 // S = −(HAH)[:n, :n] symmetric positive definite, n = N − 1) is factored S = L Lᵀ in fp64 — SciPy's fp64
 // accuracy without refinement — by a right-looking blocked Cholesky whose matrix lives in a per-workgroup
 // slot of global memory ([ld][ld] doubles, lower triangle, L2/MALL-resident while the slot is hot):
-//   per panel of NB columns: the panel rows [k0, n) are staged in LDS, the NB×NB diagonal block is
-//   factored by wave 0 (wave-synchronous), the rows below are solved against it (a triangular solve per
-//   row, one thread per row), the panel is written back, and the trailing lower triangle is updated
-//   S[i][j] −= Σ_q L[i][q]·L[j][q] in 8×8 register tiles (4 FMAs per LDS read);
+//   setup: A's row sums from every distance of a row (g = A u needs no column pass over a stored A), then
+//   S written in one pass from the distances evaluated again (write-only);
+//   per panel of NB columns: the panel rows [k0, n) are staged in LDS (a short last panel padded with the
+//   identity, so the diagonal-block code runs without per-column guards), the NB×NB diagonal block is
+//   factored in place in LDS by wave 0 (pivot inverse square roots by the fp64 rsq and two Newton steps,
+//   1 / L[c][c] kept in the panel's pitch column), the rows below are solved against it (one thread per
+//   row, multiplies by the stored reciprocals), the panel is written back, and the trailing lower
+//   triangle is updated S[i][j] −= Σ_q L[i][q]·L[j][q] in 8×4 register tiles per lane whose old values
+//   are loaded before the products;
 // then L y = [c₁ | m] and Lᵀ z = y by blocked substitutions (diagonal blocks on wave 0, the off-diagonal
-// products over the threads), the bordered elimination gives y_n and w = H y.  One workgroup per CU strides
-// over the pixels (its slot is reused pixel after pixel).  A non-positive fp64 pivot (nodes closer than
-// fp64 can separate, or repeated ones) reports RTI_ERR_SINGULAR with NaN weights, where SciPy raises
-// LinAlgError for repeated nodes.  Cost ≈ n³/3 fp64 FMAs per pixel (SciPy's LU: 2n³/3).
+// products over the threads, each thread's first backward row loaded with the diagonal block), the bordered
+// elimination gives y_n and w = H y.  One workgroup per CU strides over the pixels (its slot is reused
+// pixel after pixel; 2 or 4 smaller workgroups per CU measured slower, their slots outgrow the MALL).  A
+// non-positive fp64 pivot (nodes closer than fp64 can separate, or repeated ones) reports RTI_ERR_SINGULAR
+// with NaN weights, where SciPy raises LinAlgError for repeated nodes.  Cost ≈ n³/3 fp64 FMAs per pixel
+// (SciPy's LU: 2n³/3).
 constexpr int RBF_CH_THREADS = 512;
 constexpr size_t RBF_CH_LDS = 160 * 1024 - 256;  // dynamic LDS per workgroup (the static part is < 256 B)
 
@@ -992,15 +999,30 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
   long long prof_[16] = {}, last_ = wall_clock64();
 #endif
   // one diagonal block's two triangular solves on wave 0: lanes r and 32 + r hold row r's entries of the
-  // two right-hand sides; L[r][c] at Ld[r·LDP + c].  Forward: L z = s; backward: Lᵀ z = s.
+  // two right-hand sides; L[r][c] at Ld[r·LDP + c], 1 / L[c][c] at Ld[c·LDP + NB] (the pitch column).
+  // Forward: L z = s; backward: Lᵀ z = s.  Unrolled over NB so the block's LDS reads issue ahead of the
+  // dependent chain; z_c reaches every lane by readlane (no LDS round trip per step).
   const int r32 = lane & 31;
-  auto diag_solve = [&](const double* Ld, int kb, double* ya, double* yb, bool backward) {
+  // (the block is padded to NB with the identity and rows >= kb start at 0, so the steps run unguarded)
+  auto diag_fwd = [&](const double* Ld, int kb, double* ya, double* yb) {
     double v = r32 < kb ? (lane < 32 ? ya[r32] : yb[r32]) : 0.0;
-    for (int i = 0; i < kb; ++i) {
-      const int c = backward ? kb - 1 - i : i;
-      if (r32 == c) v /= Ld[c * LDP + c];
-      const double zc = __shfl(v, (lane & 32) + c, 64);
-      if (backward ? r32 < c : (r32 > c && r32 < kb)) v = fma(backward ? -Ld[c * LDP + r32] : -Ld[r32 * LDP + c], zc, v);
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+      const double l = Ld[r32 * LDP + c], rd = Ld[c * LDP + NB];
+      if (r32 == c) v *= rd;
+      const double z0 = readlane64(v, c), z1 = readlane64(v, 32 + c);
+      if (r32 > c) v = fma(-l, lane < 32 ? z0 : z1, v);
+    }
+    if (r32 < kb) (lane < 32 ? ya : yb)[r32] = v;
+  };
+  auto diag_bwd = [&](const double* Ld, int kb, double* ya, double* yb) {
+    double v = r32 < kb ? (lane < 32 ? ya[r32] : yb[r32]) : 0.0;
+#pragma unroll
+    for (int c = NB - 1; c >= 0; --c) {
+      const double l = Ld[c * LDP + r32], rd = Ld[c * LDP + NB];
+      if (r32 == c) v *= rd;
+      const double z0 = readlane64(v, c), z1 = readlane64(v, 32 + c);
+      if (r32 < c) v = fma(-l, lane < 32 ? z0 : z1, v);
     }
     if (r32 < kb) (lane < 32 ? ya : yb)[r32] = v;
   };
@@ -1016,82 +1038,77 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
     }
     __syncthreads();
     CH_MARK(0);
-    // A's lower triangle into M (one wave per row, coalesced) with its row sums, and the repeated-node
-    // check (SciPy: LinAlgError); each distance is evaluated once
+    // A's row sums (one wave per row; every distance of the row, so no column pass over a stored A) and the
+    // repeated-node check (SciPy: LinAlgError); g = A u = e·(row sums) − A[:, n]
     bool dup = false;
     for (int i = wave; i < N; i += TH / 64) {
       double rs = 0.0;
-      for (int j = lane; j <= i; j += 64) {
+      for (int j = lane; j < N; j += 64) {
         const double d = dist(i, j);
-        M[(int64_t)i * ld + j] = d;
         rs += d;
         dup = dup || (j != i && d == 0.0);
       }
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
-      if (lane == 0) y2[i] = rs;
+      if (lane == 0) gv[i] = fma(e, rs, -(i < n ? dist(n, i) : 0.0));
     }
     if (dup) s_bad = 1;
     __syncthreads();
     CH_MARK(1);
-    // g = A u = e·(row sums) − A[:, n]: add the upper part of each row sum (a column of the lower
-    // triangle, coalesced over i)
-    for (int i = t; i < N; i += TH) {
-      double rs = y2[i];
-      for (int j = i + 1; j < N; ++j) rs += M[(int64_t)j * ld + i];
-      gv[i] = fma(e, rs, -(i < n ? M[(int64_t)n * ld + i] : 0.0));
-    }
-    __syncthreads();
     CH_MARK(2);
     double ub = 0.0, ug = 0.0;
     for (int i = t; i < N; i += TH) ub = fma(u(i), y1[i], ub), ug = fma(u(i), gv[i], ug);
     const double utb = sum_all(ub), b2 = beta * beta * sum_all(ug);
-    // HAH from the stored distances (i >= j)
+    // HAH from the distances (i >= j)
     auto hah = [&](int i, int j, double d) { return d - beta * (u(i) * gv[j] + gv[i] * u(j)) + b2 * u(i) * u(j); };
     for (int i = t; i < N; i += TH) {
-      const double ci = y1[i] - beta * u(i) * utb, mi = hah(n, i, i < n ? M[(int64_t)n * ld + i] : 0.0);
+      const double ci = y1[i] - beta * u(i) * utb, mi = hah(n, i, i < n ? dist(n, i) : 0.0);
       cv[i] = ci, mv[i] = mi, y1[i] = ci, y2[i] = mi;
     }
-    __syncthreads();  // row n of M is read above; S overwrites rows [0, n) only, but keep the phases apart
-    // S = −(HAH)[:n, :n] in place, lower triangle, one wave per row
+    // S = −(HAH)[:n, :n] into M, lower triangle, one wave per row (the distances again: a write-only pass)
     for (int i = wave; i < n; i += TH / 64)
-      for (int j = lane; j <= i; j += 64) {
-        double* mij = M + (int64_t)i * ld + j;
-        *mij = -hah(i, j, *mij);
-      }
+      for (int j = lane; j <= i; j += 64) M[(int64_t)i * ld + j] = -hah(i, j, dist(i, j));
     __syncthreads();
     CH_MARK(3);
 
     // ---- blocked Cholesky S = L Lᵀ, with the forward substitutions L y = [c₁ | m] panel by panel --------
     for (int k0 = 0; k0 < n && !s_bad; k0 += NB) {  // s_bad: block-uniform after each sync
       const int kb = min(NB, n - k0), rows = n - k0;
-      for (int idx = t; idx < rows * NB; idx += TH) {  // stage the panel rows [k0, n), columns [k0, k0 + kb)
+      // stage the panel rows [k0, n), columns [k0, k0 + kb); a short last panel (kb < NB, then rows = kb) is
+      // padded to NB rows and columns with the identity, so the diagonal block's code below runs unguarded
+      for (int idx = t; idx < max(rows, NB) * NB; idx += TH) {
         const int r = idx / NB, c = idx - r * NB;
-        pan[r * LDP + c] = (c < kb && c <= r) ? M[(int64_t)(k0 + r) * ld + k0 + c] : 0.0;
+        pan[r * LDP + c] = (c < kb && c <= r && r < rows) ? M[(int64_t)(k0 + r) * ld + k0 + c] : (r == c && r >= kb ? 1.0 : 0.0);
       }
       __syncthreads();
       CH_MARK(4);
-      if (wave == 0) {  // the diagonal block in registers: lane r holds row r, pivots broadcast by readlane
-        double a[NB];
-#pragma unroll
-        for (int c = 0; c < NB; ++c) a[c] = r32 < kb && lane < 32 ? pan[r32 * LDP + c] : 0.0;
+      if (wave == 0 && lane < NB) {  // the diagonal block in place in LDS, lane r updating row r (right-looking):
+        // the pivot and column c of L are uniform-address (broadcast) reads, the pivot's inverse square root is
+        // the fp64 rsq with two Newton steps (no sqrt / divide chains on this serial path); 1 / L[c][c] goes to
+        // the pitch column for the solves
+        double* row = pan + lane * LDP;
         bool bad = false;
 #pragma unroll
         for (int c = 0; c < NB; ++c) {
-          if (c < kb) {
-            const double d = readlane64(a[c], c);
-            bad = bad || !(d > 0.0);
-            const double sd = sqrt(d), inv = 1.0 / sd;
-            a[c] = r32 == c ? sd : a[c] * inv;  // column c of L (rows > c), the pivot on the diagonal
+          const double d = pan[c * LDP + c];
+          bad = bad || !(d > 0.0);
+          double inv = __builtin_amdgcn_rsq(d);
+          inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
+          inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
+          if (lane == c) row[NB] = inv;
+          const double lrc = lane == c ? d * inv : row[c] * inv;  // L[r][c] (rows r >= c are used)
+          if (lane >= c) row[c] = lrc;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          double lq[NB];
 #pragma unroll
-            for (int q = c + 1; q < NB; ++q)
-              if (q < kb) a[q] = fma(-a[c], readlane64(a[c], q), a[q]);  // L[r][q] −= L[r][c]·L[q][c]
-          }
-        }
-        if (lane < 32 && r32 < kb) {
+          for (int q = c + 1; q < NB; ++q) lq[q] = pan[q * LDP + c];
 #pragma unroll
-          for (int c = 0; c < NB; ++c)
-            if (c <= r32) pan[r32 * LDP + c] = a[c];
+          for (int q = c + 1; q < NB; ++q) row[q] = fma(-lrc, lq[q], row[q]);  // L[r][q] −= L[r][c]·L[q][c]
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         if (bad && lane == 0) s_bad = 1;
       }
@@ -1100,23 +1117,18 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       if (s_bad) break;  // a non-positive pivot
       // rows below the block: x·L_Dᵀ = panel row  ->  forward substitution against the diagonal block;
       // wave 0 meanwhile solves the block's part of L y = [c₁ | m]
-      if (wave == 0) diag_solve(pan, kb, y1 + k0, y2 + k0, false);
+      if (wave == 0) diag_fwd(pan, kb, y1 + k0, y2 + k0);
       for (int r = kb + t; r < rows; r += TH) {
         double x[NB];
 #pragma unroll
-        for (int c = 0; c < NB; ++c) {
-          if (c < kb) {
-            double s = pan[r * LDP + c];
+        for (int c = 0; c < NB; ++c) {  // (rows below the block exist only when kb = NB)
+          double s = pan[r * LDP + c];
 #pragma unroll
-            for (int q = 0; q < c; ++q) s = fma(-x[q], pan[c * LDP + q], s);
-            x[c] = s / pan[c * LDP + c];
-          } else {
-            x[c] = 0.0;
-          }
+          for (int q = 0; q < c; ++q) s = fma(-x[q], pan[c * LDP + q], s);
+          x[c] = s * pan[c * LDP + NB];
         }
 #pragma unroll
-        for (int c = 0; c < NB; ++c)
-          if (c < kb) pan[r * LDP + c] = x[c];
+        for (int c = 0; c < NB; ++c) pan[r * LDP + c] = x[c];
       }
       __syncthreads();
       CH_MARK(6);
@@ -1127,12 +1139,10 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       for (int r = kb + t; r < rows; r += TH) {  // y[i] −= L[i][k0:k0+kb]·y_block (LDS)
         double s1 = y1[k0 + r], s2 = y2[k0 + r];
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-          if (q < kb) {
-            const double l = pan[r * LDP + q];
-            s1 = fma(-l, y1[k0 + q], s1);
-            s2 = fma(-l, y2[k0 + q], s2);
-          }
+        for (int q = 0; q < NB; ++q) {  // (kb = NB here, as above)
+          const double l = pan[r * LDP + q];
+          s1 = fma(-l, y1[k0 + q], s1);
+          s2 = fma(-l, y2[k0 + q], s2);
         }
         y1[k0 + r] = s1, y2[k0 + r] = s2;
       }
@@ -1149,11 +1159,18 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         const int J32 = st - I64 * (I64 + 1);
         const int ri = kb + 64 * I64 + ly, rj = kb + 32 * J32 + lx;
         if (32 * J32 >= m) continue;  // past the trailing block (the last row tile's right half)
-        double acc[8][4];
+        // the tile's old values are loaded ahead of the products (their latency hides behind the FMAs)
+        double acc[8][4], old[8][4];
 #pragma unroll
-        for (int a = 0; a < 8; ++a)
+        for (int a = 0; a < 8; ++a) {
+          const int rr = min(ri + 8 * a, rows - 1);
+          const double* row = M + (int64_t)(k0 + rr) * ld + k0;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+          for (int b = 0; b < 4; ++b) {
+            acc[a][b] = 0.0;
+            old[a][b] = row[min(rj + 8 * b, rr)];  // clamped into the stored lower triangle
+          }
+        }
         for (int q = 0; q < kb; ++q) {
           double li[8], lj[4];
 #pragma unroll
@@ -1171,7 +1188,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
           double* row = M + (int64_t)(k0 + ri + 8 * a) * ld + k0;
 #pragma unroll
           for (int b = 0; b < 4; ++b)
-            if (rj + 8 * b < rows && rj + 8 * b <= ri + 8 * a) row[rj + 8 * b] -= acc[a][b];
+            if (rj + 8 * b < rows && rj + 8 * b <= ri + 8 * a) row[rj + 8 * b] = old[a][b] - acc[a][b];
         }
       }
       __syncthreads();
@@ -1185,27 +1202,35 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       continue;
     }
     // ---- Lᵀ z = y (backward), blocked by NB: diagonal blocks staged in LDS (the panel is free) --------
+    // Each thread's first row of the off-diagonal update (i = t) is loaded with the diagonal block, so one
+    // global-memory latency per block sits on the serial path.
     for (int k0 = (n - 1) / NB * NB; k0 >= 0; k0 -= NB) {
       const int kb = min(NB, n - k0);
-      for (int idx = t; idx < kb * NB; idx += TH) {
+      double lp[NB];
+#pragma unroll
+      for (int q = 0; q < NB; ++q) lp[q] = t < k0 ? M[(int64_t)(k0 + min(q, kb - 1)) * ld + t] : 0.0;
+      for (int idx = t; idx < NB * NB; idx += TH) {  // (a short block padded with the identity)
         const int r = idx / NB, c = idx - r * NB;
-        if (c <= r) pan[r * LDP + c] = M[(int64_t)(k0 + r) * ld + k0 + c];
+        const double l = r < kb && c <= r ? M[(int64_t)(k0 + r) * ld + k0 + c] : (r == c ? 1.0 : 0.0);
+        pan[r * LDP + c] = l;
+        if (c == r) pan[r * LDP + NB] = 1.0 / l;
       }
       __syncthreads();
-      if (wave == 0) diag_solve(pan, kb, y1 + k0, y2 + k0, true);
+      if (wave == 0) diag_bwd(pan, kb, y1 + k0, y2 + k0);
       __syncthreads();
-      for (int i = t; i < k0; i += TH) {  // y[i] −= Σ_q L[k0+q][i]·z[k0+q]: rows of L, coalesced over i
+      // y[i] −= Σ_q L[k0+q][i]·z[k0+q]: rows of L, coalesced over i (z = 0 past a short block's end)
+      auto upd = [&](int i, auto&& lval) {
         double s1 = y1[i], s2 = y2[i];
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          if (q < kb) {
-            const double l = M[(int64_t)(k0 + q) * ld + i];
-            s1 = fma(-l, y1[k0 + q], s1);
-            s2 = fma(-l, y2[k0 + q], s2);
-          }
+          const double l = lval(q), z1 = q < kb ? y1[k0 + q] : 0.0, z2 = q < kb ? y2[k0 + q] : 0.0;
+          s1 = fma(-l, z1, s1);
+          s2 = fma(-l, z2, s2);
         }
         y1[i] = s1, y2[i] = s2;
-      }
+      };
+      if (t < k0) upd(t, [&](int q) { return lp[q]; });
+      for (int i = t + TH; i < k0; i += TH) upd(i, [&](int q) { return M[(int64_t)(k0 + min(q, kb - 1)) * ld + i]; });
       __syncthreads();
     }
     CH_MARK(9);

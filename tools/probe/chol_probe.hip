@@ -10,6 +10,16 @@
 #include <random>
 #include <vector>
 
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I smartphone-based-rti_amd/csrc
+//        tools/probe/chol_probe.hip smartphone-based-rti_amd/csrc/rti_host.cpp -o tools/probe/chol_probe
+namespace rti {
+int device_cus() {  // librti's lives in rti_fit.hip
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  return cus;
+}
+}  // namespace rti
+
 int main(int argc, char** argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 400;
   const int64_t P = argc > 2 ? atoll(argv[2]) : 2560;
