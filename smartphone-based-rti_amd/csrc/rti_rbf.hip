@@ -1117,8 +1117,9 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       if (s_bad) break;  // a non-positive pivot
       // rows below the block: x·L_Dᵀ = panel row  ->  forward substitution against the diagonal block;
       // wave 0 meanwhile solves the block's part of L y = [c₁ | m]
+      // (waves 1.. take the rows, so wave 0's serial block solve is not followed by a share of them)
       if (wave == 0) diag_fwd(pan, kb, y1 + k0, y2 + k0);
-      for (int r = kb + t; r < rows; r += TH) {
+      for (int r = kb + t - 64; wave > 0 && r < rows; r += TH - 64) {
         double x[NB];
 #pragma unroll
         for (int c = 0; c < NB; ++c) {  // (rows below the block exist only when kb = NB)
