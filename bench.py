@@ -167,7 +167,7 @@ def synth_cams(n, seed, H, W):
 # is reported only while these files are byte-identical to the ones the counters were taken on
 KERNEL_SOURCES = {
     "fit_shared_valu": ["rti_fit.hip"], "fit_shared_tile": ["rti_fit.hip"], "fit_shared_mfma": ["rti_fit.hip"],
-    "fit_q8": ["rti_fit_q8.hip", "rti_q8.h"], "fit_h16": ["rti_fit_h16.hip"], "fit_shared_residual_k": ["rti_fitres.hip"],
+    "fit_q8": ["rti_fit_q8.hip", "rti_q8.h"], "fit_pm": ["rti_fit_pm.hip"], "fit_h16": ["rti_fit_h16.hip"], "fit_shared_residual_k": ["rti_fitres.hip"],
     "fit_residual_k": ["rti_residual.hip"], "relight_eval": ["rti_relight.hip", "rti_convert.h"],
     "relight_frame": ["rti_relight.hip", "rti_convert.h"], "fit_perpixel_cam": ["rti_perpixel.hip"],
     "apply_op": ["rti_operator.hip"], "rbf_": ["rti_rbf.hip"],
@@ -232,6 +232,12 @@ def sample_idx(P, n, seed):
     if P <= n:
         return np.arange(P)
     return np.sort(rng.choice(P, n, replace=False))
+
+
+def torch_idx(idx, device):
+    import torch
+
+    return torch.as_tensor(idx, device=device)
 
 
 def coef_parity(got, ref):
@@ -304,6 +310,9 @@ class FitWorkload(Workload):
         if args.in_dtype != "f32":  # integer-valued 0..255 stacks, as the reference's V channel (analysis.py:219)
             self.I = self.I.to(torch.uint8 if args.in_dtype == "u8" else torch.int32)
             self.in_bytes = 1 if args.in_dtype == "u8" else 4
+        self.stack = getattr(args, "stack", "light")
+        if self.stack == "pixel":  # the reference's own (R, R, N) layout (analysis.py:217-219): I[c][p][n]
+            self.I = self.I.transpose(1, 2).contiguous()
         self.pinv64 = rti.pinv(self.lu, self.lv, basis)
         self.pinv_dev = torch.as_tensor(self.pinv64.astype(np.float32), device=dev)
         self.coef = torch.empty((C, P, k) if args.layout == "pixel" else (C, k, P), dtype=torch.float32, device=dev)
@@ -319,7 +328,7 @@ class FitWorkload(Workload):
         # 8-bit stacks: rti.fit's AUTO path, the split-fp16 fit on the fp16 matrix cores (rti_fit_h16.hip), or
         # with --kernel q8 the int8 fixed-point form (rti_fit_q8.hip)
         mk = "h16" if args.kernel == "auto" else args.kernel
-        self.q8 = mk in ("h16", "q8") and rti.api.q8_supported(self.I, k, N, P, mk)
+        self.q8 = self.stack == "light" and mk in ("h16", "q8") and rti.api.q8_supported(self.I, k, N, P, mk)
         self.u8_kernel = mk if self.q8 else None
         if self.q8:
             if mk == "h16":
@@ -330,6 +339,13 @@ class FitWorkload(Workload):
                 fn, fname = L.lib().rti_fit_shared_q8, "rti_fit_shared_q8"
             cargs = (ctypes.c_void_p(self.op_dev.data_ptr()), k, N, ctypes.c_void_p(self.I.data_ptr()), P, C, P, N * P,
                      ctypes.c_void_p(self.coef.data_ptr()), rti.api._layout_id(args.layout), P * k, 0, stream)
+        elif self.stack == "pixel":  # rti_fit_shared_pm: pixel stride N, channel stride P·N
+            fn, fname = L.lib().rti_fit_shared_pm, "rti_fit_shared_pm"
+            cargs = (ctypes.c_void_p(self.pinv_dev.data_ptr()), k, N, ctypes.c_void_p(self.I.data_ptr()),
+                     rti.api._IN_DTYPES[self.I.dtype], P, C, N, P * N, ctypes.c_void_p(self.coef.data_ptr()),
+                     rti.api._layout_id(args.layout), P * k, rti.api._KERNELS[args.kernel], stream)
+            self.pm_plan = int(L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[self.I.dtype], P, C, N, P * N,
+                                                              rti.api._KERNELS[args.kernel]))
         else:
             kern = rti.api._KERNELS[args.kernel] | (L.RTI_KERNEL_NONTEMPORAL if args.nontemporal else 0)
             fn, fname = L.lib().rti_fit_shared, "rti_fit_shared"
@@ -354,13 +370,23 @@ class FitWorkload(Workload):
         if self.ctx.world != 1 or self.ctx.weak:
             return None  # the PMC figures in profiles/traffic.json are for the whole image
         a = self.args
-        key = f"{a.config}-{a.kernel}-{a.layout}" + ("" if a.in_dtype == "f32" else f"-{a.in_dtype}")
-        return load_traffic(key, f"fit_{self.u8_kernel}" if self.u8_kernel else None)
+        key = f"{a.config}-{a.kernel}-{a.layout}" + ("" if a.in_dtype == "f32" else f"-{a.in_dtype}") + \
+            ("-pm" if self.stack == "pixel" else "")
+        fam = f"fit_{self.u8_kernel}" if self.u8_kernel else ("fit_pm" if self.stack == "pixel" else None)
+        return load_traffic(key, fam)
 
     def config(self):
-        return {"lights": self.N, "channels": self.C, "basis": self.basis, "k": self.k,
-                "coef_layout": self.args.layout, "kernel": self.u8_kernel or self.args.kernel,
-                "intensity_dtype": self.args.in_dtype}
+        cfg = {"lights": self.N, "channels": self.C, "basis": self.basis, "k": self.k,
+               "coef_layout": self.args.layout, "kernel": self.u8_kernel or self.args.kernel,
+               "intensity_dtype": self.args.in_dtype, "stack_layout": self.stack}
+        if self.stack == "pixel":
+            cfg["pm_plan"] = {"pixels_per_block": self.pm_plan // 1000, "waves_per_cu": self.pm_plan % 1000} \
+                if self.pm_plan else "one lane per pixel"
+        return cfg
+
+    def stack_cols(self, c, idx):
+        """[N, len(idx)] intensities of channel c at pixels idx, whatever the stack layout."""
+        return self.I[c][idx, :].T if self.stack == "pixel" else self.I[c][:, idx]
 
     def coef_pk(self, c):
         cc = self.coef[c]
@@ -371,7 +397,7 @@ class FitWorkload(Workload):
         idx = sample_idx(self.P, 4096, 11 + self.ctx.rank)
         worst = 0.0
         for c in sorted({0, self.C - 1}):
-            I = self.I[c][:, idx].float().cpu().numpy()
+            I = self.stack_cols(c, torch_idx(idx, self.I.device)).float().cpu().numpy()
             ref = o.fit_shared(I, self.pinv64)
             got = self.coef_pk(c)[idx].cpu().numpy()
             worst = max(worst, coef_parity(got, ref))
@@ -381,7 +407,8 @@ class FitWorkload(Workload):
     def cpu_fn(self):
         o = oracle()
         rows = max(1, min(self.ctx.h, 216))
-        sample = self.I[0, :, : rows * self.W].float().cpu().numpy()
+        sample = (self.I[0, : rows * self.W, :].T if self.stack == "pixel" else self.I[0, :, : rows * self.W]).float()
+        sample = np.ascontiguousarray(sample.cpu().numpy())
         return (lambda: o.fit_shared_f32(sample, self.pinv64), self.N * rows * self.W,
                 f"oracle fit_shared_f32 (fp64 pinv + fp32 NumPy matmul, channel 0) on {rows}x{self.W} px x {self.N} "
                 f"lights")
@@ -1025,6 +1052,8 @@ def parse_args(argv=None):
     ap.add_argument("--weak", action="store_true", help="every rank fits a whole H-row image (weak scaling)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma", "tile", "q8", "h16"])
     ap.add_argument("--layout", default="pixel", choices=["pixel", "planar"])
+    ap.add_argument("--stack", default="light", choices=["light", "pixel"],
+                    help="fit configs: intensity stack layout; pixel = the reference's (R, R, N) (rti_fit_shared_pm)")
     ap.add_argument("--nontemporal", action="store_true")
     ap.add_argument("--in-dtype", default="f32", choices=["f32", "u8", "i32"],
                     help="intensity stack type for fit configs (BASELINE's metric is fp32)")
@@ -1053,6 +1082,8 @@ def main():
         h, w = (int(x) for x in args.shape.lower().split("x"))
         cfg = (cfg[0], h, w) + cfg[3:6] + (cfg[6] + f" [shape override {h}x{w}]",)
     kind = cfg[0]
+    if args.stack == "pixel" and kind != "fit":
+        raise SystemExit("--stack pixel applies to the fit configs (c2, c3, c4)")
     if args.steps is None:
         args.steps = DEFAULT_STEPS[kind]
 

@@ -20,8 +20,8 @@
  *   - Reentrant: no global mutable state besides the thread-local message.
  *   - Intensity stacks are LIGHT-MAJOR: I[c][n][p] with pixel p = y*W + x
  *     contiguous inside one light plane (strides in elements; 0 = dense).
- *     The reference stacks pixel-major [y][x][n] (analysis.py:217-219); the
- *     per-pixel "dirs" entry point accepts that layout.
+ *     The reference stacks pixel-major [y][x][n] (analysis.py:217-219);
+ *     rti_fit_shared_pm and the per-pixel "dirs" entry point take that layout.
  */
 #ifndef RTI_H
 #define RTI_H
@@ -68,7 +68,7 @@ extern "C" {
 #define RTI_KERNEL_PINV_LDS    0x200  /* stage pinv in LDS instead of scalar loads */
 #define RTI_KERNEL_NT_STORE    0x400  /* non-temporal coefficient stores */
 #define RTI_KERNEL_STAGE       0x800  /* pixel-major output transposed through LDS (1 KiB stores) */
-#define RTI_KERNEL_ROTATE      0x10000000  /* AUTO PTM-6 fp32: each wave starts its light sweep at its own plane (measurement variant) */
+#define RTI_KERNEL_ROTATE      0x10000000  /* AUTO PTM-6 fp32: each wave starts its light sweep at its own plane; rti_fit_shared_pm: each wave streams one contiguous run of units (measurement variants) */
 #define RTI_KERNEL_ROUNDS      0x40000000  /* AUTO PTM-6 fp32/int32: launch generations as rounds of one launch (rti_fit.hip) */
 #define RTI_KERNEL_ONE_LAUNCH  0x20000000  /* AUTO: one launch, no launch generations (measurement variant; rti_fit.hip) */
 /* VALU chunks per lane (bits 12-15; 0 = AUTO): a wave reads chunks*1 KiB contiguous per plane */
@@ -139,6 +139,28 @@ int rti_fit_shared(const float* pinv, int k, int N,
                    int64_t light_stride, int64_t channel_stride,
                    float* coef, int coef_layout, int64_t coef_channel_stride,
                    int kernel, rti_stream_t stream);
+
+/* ---- device: shared-direction fit on PIXEL-major stacks (rti_fit_pm.hip) ---------------
+ * The same contraction as rti_fit_shared on the reference's own stack layout: compute_intensities
+ * returns (R, R, N) arrays (analysis.py:217-219), pixel p's N intensities contiguous:
+ *   coef[c][p][i] = Σ_n pinv[i][n] · I[c*channel_stride + p*pixel_stride + n]
+ * (pixel_stride 0 = N, channel_stride 0 = P*pixel_stride).  pinv, coef, coef_layout and
+ * coef_channel_stride as rti_fit_shared; in_dtype F32 / I32 / U8.
+ * AUTO (and RTI_KERNEL_MFMA) streams whole blocks of 16·G consecutive pixels (one contiguous run of
+ * 16·G·N values) HBM -> LDS by LDS-DMA and contracts them with v_mfma_f32_16x16x4_f32: F32 / I32 stacks,
+ * k in {6, 9, 16}, pixel_stride = N, P·N and channel_stride multiples of 4, I and coef 16-byte aligned,
+ * P·k·4 < 2^31 and N within the LDS budget (rti_fit_shared_pm_plan).  RTI_KERNEL_MFMA fails with
+ * RTI_ERR_UNSUPPORTED outside that; AUTO and RTI_KERNEL_VALU run one lane per pixel instead (any shape).
+ * kernel: RTI_KERNEL_CHUNKS(G) (G in {1, 2, 4}) and RTI_KERNEL_TILE_WAVES(W) override the block and the
+ * waves per workgroup (measurement). */
+int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
+                      int64_t pixel_stride, int64_t channel_stride,
+                      float* coef, int coef_layout, int64_t coef_channel_stride,
+                      int kernel, rti_stream_t stream);
+/* 0 if rti_fit_shared_pm's DMA/MFMA kernel does not take this shape, else its plan:
+ * 1000·(pixels per block) + waves per workgroup. */
+int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int C, int64_t pixel_stride,
+                           int64_t channel_stride, int kernel);
 
 /* ---- 8-bit stacks: the shared fit on the int8 matrix cores -------------------------
  * The reference's intensities are the uint8 V channel (FeatureMatcher.py:183-184, analysis.py:219).

@@ -1,0 +1,942 @@
+// rti_fit_pm.hip -- the shared-direction fit on PIXEL-major stacks, the reference's own layout.
+//
+// compute_intensities stacks the ROI as (R, R, N) (analysis.py:217-219): the N intensities of a
+// pixel are contiguous.  For a shared light set the solve of analysis.py:293-298 is the same
+// contraction as rti_fit.hip's,
+//     coef[c][p][i] = Σ_n pinv[i][n] · I[c][p][n],
+// but the operand arrives transposed.  A block of B consecutive pixels is then ONE contiguous run
+// of B·N values, which is the best shape the HBM stream can ask for: the kernel copies whole
+// blocks into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, no VGPR hop)
+// and contracts them on the matrix cores.
+//
+//  * fit_pm_dma: every wave owns a private double-buffered LDS ring of two blocks of B pixels
+//    (B = 16, 32 or 64).  A wave waits for its block, issues the DMA of its next block (grid-
+//    strided over the flattened (channel, block) space), then runs v_mfma_f32_16x16x4_f32 with
+//    A = pinv (row i of the [16][N16] zero-padded operator in LDS: lane (q, r) reads
+//    pinv[q][16m + 4r .. +3] with one ds_read_b128) and B = the block (lane (q, r) reads
+//    I[p0 + q][16m + 4r .. +3]), four MFMAs per 16 lights: D[i][j] is coefficient i of pixel j.
+//    The waves never synchronise with each other: each DMA is waited for by a counted vmcnt that
+//    leaves the previous block's coefficient stores in flight (CDNA retires loads and stores on
+//    one counter in issue order), so those stores are issued unconditionally as buffer stores
+//    whose out-of-range lanes the buffer bounds drop.
+//  * fit_pm_lane: one lane per pixel, the k×N operator in SGPRs, per-lane loads of the pixel's
+//    row.  For what the DMA kernel does not take (uint8 stacks, a pixel stride other than N,
+//    unaligned shapes, N past the LDS budget).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "rti_internal.h"
+
+namespace rti {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef int intx4 __attribute__((ext_vector_type(4)));
+typedef int intx2 __attribute__((ext_vector_type(2)));
+
+constexpr int PM_LDS = 160 * 1024;
+constexpr uint32_t PM_OOB = 0x80000000u;  // buffer offset past every num_records: the store is dropped
+constexpr uint32_t PM_OOB_ALL = 0xFFFFFFF0u;  // the same for a buffer over the whole coefficient array (< 2^32 - 16 B)
+
+__device__ __forceinline__ void dma16(const void* g, float* lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 2 /* nt */);
+}
+
+template <typename T>
+__device__ __forceinline__ float to_f(T v) {
+  return (float)v;
+}
+
+// 4 consecutive values of the LDS block at float offset `o` (aligned to ALIGN floats)
+template <int ALIGN, typename T>
+__device__ __forceinline__ floatx4 lds4(const float* blk, int o) {
+  const T* b = reinterpret_cast<const T*>(blk);
+  if constexpr (ALIGN == 4) {
+    typedef T tx4 __attribute__((ext_vector_type(4)));
+    const tx4 v = *reinterpret_cast<const tx4*>(b + o);
+    return floatx4{to_f(v[0]), to_f(v[1]), to_f(v[2]), to_f(v[3])};
+  } else if constexpr (ALIGN == 2) {
+    typedef T tx2 __attribute__((ext_vector_type(2)));
+    const tx2 u = *reinterpret_cast<const tx2*>(b + o), v = *reinterpret_cast<const tx2*>(b + o + 2);
+    return floatx4{to_f(u[0]), to_f(u[1]), to_f(v[0]), to_f(v[1])};
+  } else {
+    return floatx4{to_f(b[o]), to_f(b[o + 1]), to_f(b[o + 2]), to_f(b[o + 3])};
+  }
+}
+
+// Coefficient stores of one 16-pixel group: lane (q, r) holds coefficients 4r .. 4r+3 of pixel px.
+// Every lane issues the same S_GROUP instructions; those of absent coefficients or pixels get an
+// out-of-range offset.  Offsets are bytes inside the channel's coefficient buffer (< 2^31).
+template <int K, int LAYOUT>
+constexpr int stores_per_group() {
+  if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR) return K % 4 == 0 ? 1 : (K % 2 == 0 ? 2 : 4);
+  return 4;
+}
+
+template <int K, int LAYOUT>
+__device__ __forceinline__ void store_group(__amdgpu_buffer_rsrc_t rs, floatx4 d, int64_t px, int64_t P, int r) {
+  const bool pin = px < P;
+  if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 4 == 0) {
+    const uint32_t off = (pin && 4 * r < K) ? (uint32_t)((px * K + 4 * r) * 4) : PM_OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(intx4, d), rs, off, 0, 0);
+  } else if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = 4 * r + 2 * h;
+      const uint32_t off = (pin && i < K) ? (uint32_t)((px * K + i) * 4) : PM_OOB;
+      const floatx2 v = h == 0 ? floatx2{d[0], d[1]} : floatx2{d[2], d[3]};
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(intx2, v), rs, off, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int i = 4 * r + rr;
+      const int64_t e = LAYOUT == RTI_COEF_PIXEL_MAJOR ? px * K + i : (int64_t)i * P + px;
+      const uint32_t off = (pin && i < K) ? (uint32_t)(e * 4) : PM_OOB;
+      const float v = d[rr];  // (a bit_cast of the vector element itself reads element 0: clang, ROCm 7.2)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), rs, off, 0, 0);
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// BP pixels per block (16·G), K coefficients (<= 16), T = float / int32_t, ALIGN = the alignment of a
+// pixel row in floats (4: N % 4 == 0 -> ds_read_b128; 2; 1).  Dynamic LDS: [16][N16] operator, then
+// per wave two blocks of `slot` floats.
+template <int G, int K, typename T, int LAYOUT, int ALIGN>
+__global__ void __launch_bounds__(512)
+fit_pm_dma(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
+           float* __restrict__ coef, int64_t ocstride, int64_t nblk, int64_t units, int slot) {
+  constexpr int BP = 16 * G;
+  constexpr int S = G * stores_per_group<K, LAYOUT>();  // store instructions per block (compile-time)
+  static_assert(S <= 63, "vmcnt immediate");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int N16 = (N + 15) & ~15;
+  const int W = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar block walk
+  float* __restrict__ lp = lds;  // [16][N16]
+  for (int idx = threadIdx.x; idx < 16 * N16; idx += blockDim.x) {
+    const int i = idx / N16, n = idx - i * N16;
+    lp[idx] = (i < K && n < N) ? pinv[i * N + n] : 0.f;
+  }
+  __syncthreads();
+  float* __restrict__ ring = lds + 16 * N16 + wave * 2 * slot;
+  const int64_t gw = (int64_t)blockIdx.x * W + wave, GW = (int64_t)gridDim.x * W;
+  if (gw >= units) return;
+  const int64_t bbytes = (int64_t)BP * N * sizeof(T), cbytes = P * N * (int64_t)sizeof(T);
+  const int L = (int)((bbytes + 1023) >> 10);  // DMA instructions per block
+  auto issue = [&](int64_t u, int s) {
+    const int64_t c = u / nblk, b = u - c * nblk;
+    const char* base = reinterpret_cast<const char*>(I + c * cstride);
+    int64_t off = b * bbytes + 16 * lane;
+    float* dst = ring + s * slot;
+    for (int i = 0; i < L; ++i, off += 1024)  // lanes past the channel re-read its last 16 B (never used)
+      dma16(base + (off + 16 <= cbytes ? off : cbytes - 16), dst + i * 256);
+  };
+  const int q = lane & 15, r = lane >> 4;
+  const int nfull = N >> 4;  // whole 16-light chunks; a partial last chunk is masked
+  issue(gw, 0);
+  int s = 0;
+  bool first = true;
+  for (int64_t u = gw; u < units; u += GW) {
+    // this block's DMAs were issued before the previous block's S stores
+    if (first) wait_vm<0>(); else wait_vm<S>();
+    first = false;
+    if (u + GW < units) issue(u + GW, s ^ 1);
+    const float* __restrict__ blk = ring + s * slot;
+    floatx4 acc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+    int o = q * N + 4 * r;  // pixel q of group 0, lights 4r.. of chunk 0 (T elements)
+    for (int m = 0; m < nfull; ++m, o += 16) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(lp + q * N16 + 16 * m + 4 * r);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const floatx4 x = lds4<ALIGN, T>(blk, o + 16 * g * N);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], x[c], acc[g], 0, 0, 0);
+      }
+    }
+    if (N & 15) {  // lights 16·nfull .. N-1; the rest of the chunk reads the next pixel's values: zeroed
+      const int n0 = 16 * nfull + 4 * r;
+      const floatx4 a = *reinterpret_cast<const floatx4*>(lp + q * N16 + 16 * nfull + 4 * r);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        floatx4 x = lds4<1, T>(blk, o + 16 * g * N);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[c] = n0 + c < N ? x[c] : 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], x[c], acc[g], 0, 0, 0);
+      }
+    }
+    const int64_t c = u / nblk, p0 = (u - c * nblk) * BP;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef + c * ocstride, (short)0,
+                                                                        (int)(P * K * 4), 0x00020000);
+#pragma unroll
+    for (int g = 0; g < G; ++g) store_group<K, LAYOUT>(rs, acc[g], p0 + 16 * g + q, P, r);
+    s ^= 1;
+  }
+}
+
+// s_waitcnt vmcnt(m) for the largest m of {0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48} <= n (waiting for more
+// than needed is safe; n is wave-uniform)
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+  if (n >= 16) {
+    if (n >= 32) {
+      if (n >= 48) wait_vm<48>(); else wait_vm<32>();
+    } else {
+      if (n >= 24) wait_vm<24>(); else wait_vm<16>();
+    }
+  } else if (n >= 4) {
+    if (n >= 8) {
+      if (n >= 12) wait_vm<12>(); else wait_vm<8>();
+    } else {
+      if (n >= 6) wait_vm<6>(); else wait_vm<4>();
+    }
+  } else if (n >= 2) {
+    if (n >= 3) wait_vm<3>(); else wait_vm<2>();
+  } else if (n == 1) {
+    wait_vm<1>();
+  } else {
+    wait_vm<0>();
+  }
+}
+
+// Streaming form (AUTO).  The pixels are cut into UNITS of U 16-pixel groups, U = 16 / gcd(N, 16) (or a
+// multiple), the fewest whose bytes (16·U·N values) are a whole number of KiB, so no 1-KiB LDS-DMA
+// straddles two units and a lane's source pointer just advances by 1 KiB per DMA inside a unit.
+// Wave w of the grid owns the units w, w + GW, w + 2·GW, … of the flattened (channel, unit) space
+// (interleaved: at any moment the chip reads one contiguous slab of the stack, as the light-major fits do;
+// `contig` = 1 gives each wave one contiguous run of units instead, for A/B) and streams them, as one
+// virtual byte stream, HBM -> a private LDS ring of `ring` bytes, keeping the ring full: after each group
+// it refills every KiB the consumed groups freed, so ≈ ring − 64N bytes per wave stay in flight (the
+// double-buffered block form above keeps half its LDS in flight).  Group j of the stream occupies stream
+// bytes [64N·j, 64N·(j+1)) (fp32/int32); element (q, n) sits at ring byte (64N·j + 4(qN + n)) mod ring.
+// Before group j, the wave waits for the DMA holding its last byte, d = ⌈64N(j+1)/1024⌉ − 1, with an
+// exact count of the vector-memory ops issued after it: the DMAs issued after d, plus the S stores of
+// every group finished after d was issued (d was issued by the refill after group g(d), or by the prologue).
+// NCH > 0: at most NCH 16-light chunks (N <= 16·NCH), fully unrolled with wave-uniform guards: the
+// operator's A fragments live in VGPRs (read once from LDS) and every chunk's B reads of a group are issued
+// before its first MFMA; NCH = 0: any N, one chunk per loop step with A from LDS.
+template <int K, typename T, int LAYOUT, int ALIGN, int NCH>
+__global__ void __launch_bounds__(512)
+fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
+              float* __restrict__ coef, int64_t ocstride, int C, int U, int nu, int64_t tu, int ring, int contig) {
+  constexpr int S = stores_per_group<K, LAYOUT>();
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int N16 = (N + 15) & ~15;
+  const int W = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* __restrict__ lp = lds;  // [16][N16]
+  for (int idx = threadIdx.x; idx < 16 * N16; idx += blockDim.x) {
+    const int i = idx / N16, n = idx - i * N16;
+    lp[idx] = (i < K && n < N) ? pinv[i * N + n] : 0.f;
+  }
+  __syncthreads();
+  char* __restrict__ rp = reinterpret_cast<char*>(lds + 16 * N16) + wave * ring;
+  const int64_t gw = (int64_t)blockIdx.x * W + wave, GW = (int64_t)gridDim.x * W;
+  const int GBY = 16 * N * (int)sizeof(T);  // bytes of one 16-pixel group
+  const int64_t cbytes = P * N * (int64_t)sizeof(T);
+  const int q = lane & 15, r = lane >> 4;
+  const int nch = N16 >> 4;                        // 16-light chunks, the last one partial if N % 16
+  const int slots = ring >> 10;
+  // lane's validity of the 4 lights it reads in the last chunk (the rest belongs to the next pixel)
+  const int nlast = N - 16 * (nch - 1) - 4 * r;    // valid lights of the lane's 4 in the last chunk
+  const float* __restrict__ lpq = lp + q * N16 + 4 * r;
+  floatx4 areg[NCH > 0 ? NCH : 1];
+  if constexpr (NCH > 0) {
+#pragma unroll
+    for (int m = 0; m < NCH; ++m)
+      if (m < nch) areg[m] = *reinterpret_cast<const floatx4*>(lpq + 16 * m);
+  }
+  // this wave's units: k = 0 .. nk-1 -> global unit gu(k)
+  int64_t u0, ustep, nk;
+  if (contig) {
+    const int64_t per = (tu + GW - 1) / GW;
+    u0 = gw * per;
+    ustep = 1;
+    nk = u0 >= tu ? 0 : (tu - u0 < per ? tu - u0 : per);
+  } else {
+    u0 = gw;
+    ustep = GW;
+    nk = gw >= tu ? 0 : (tu - 1 - gw) / GW + 1;
+  }
+  if (nk == 0) return;
+  // 32-bit stream counters (SALU has no 64-bit ordered compare): a wave streams < 2 GiB, far below the
+  // 288 GB / (one wave per SIMD) of the largest stack; unit indices < nu < 2^31
+  const int ng = (int)(nk * U);                 // groups of the stream
+  const int dt = (int)(nk * ((U * GBY) >> 10));  // DMAs of the stream
+  const int ust = (int)ustep;
+  // DMA cursor: unit ud of channel cd, `left` DMAs of it still to issue, the lane's 64-bit source pointer
+  // gp (advanced by 1 KiB per DMA, rebuilt at unit changes) and the lane's last readable address gend (the
+  // channel's last 16 B: lanes past the channel re-read them, unused), ring byte wslot
+  int cd = (int)(u0 / nu), ud = (int)(u0 - (int64_t)cd * nu);
+  int cg = cd, ug = ud;  // group cursor (below): unit ug of channel cg, group gi within the unit
+  const int UB = U * GBY, UKB = UB >> 10;
+  const char* gp;
+  const char* gend;
+  auto seek = [&]() {
+    const char* ch = reinterpret_cast<const char*>(I + cd * cstride);
+    gp = ch + (int64_t)ud * UB + 16 * lane;
+    gend = ch + cbytes - 16;
+  };
+  seek();
+  int left = UKB, wslot = 0;
+  auto issue = [&]() {
+    dma16(gp < gend ? gp : gend, reinterpret_cast<float*>(rp + wslot));
+    gp += 1024;
+    wslot += 1024;
+    wslot = wslot == ring ? 0 : wslot;
+    if (--left == 0) {  // next unit (no division: ustep = GW or 1 is far below nu in practice)
+      left = UKB;
+      ud += ust;
+      while (ud >= nu) {
+        ud -= nu;
+        ++cd;
+      }
+      if (cd < C) seek();
+    }
+  };
+  int issued = dt < slots ? dt : slots;
+  for (int d = 0; d < issued; ++d) issue();
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef + (int64_t)cg * ocstride, (short)0,
+                                                                (int)(P * K * 4), 0x00020000);
+  int gi = 0;
+  int px0 = ug * U * 16;  // first pixel of group j (< P·... < 2^31)
+  int base = 0;           // ring byte of group j's first byte
+  int gd = -1;            // the refill (group index; -1 = prologue) that issued the DMA group j waits for
+  int end = 0;            // stream bytes of groups 0..j
+  const int e0b = (q * N + 4 * r) * (int)sizeof(T);  // the lane's first byte in a group
+  for (int j = 0; j < ng; ++j) {
+    end += GBY;
+    const int dn = ((end + 1023) >> 10) - 1;
+    // the refill after group g issues DMAs up to ((g+1)·GBY + ring)/1 KiB (prologue: ring/1 KiB)
+    while (((GBY * (gd + 1) + ring) >> 10) < dn + 1) ++gd;
+    const int nwait = (issued - 1 - dn) + S * (j - 1 - gd);
+    wait_vm_dyn(nwait > 63 ? 63 : nwait);
+    int a0 = base + e0b;  // ring byte of the lane's first value, chunks 64·sizeof(T)/4 bytes apart
+    a0 -= a0 >= ring ? ring : 0;
+    auto rdx = [&](int m) -> floatx4 {  // the lane's 4 values of chunk m (ring wrap per 16 B, or per value)
+      if constexpr (ALIGN == 4) {
+        int a = a0 + 16 * (int)sizeof(T) * m;
+        a -= a >= ring ? ring : 0;
+        return lds4<4, T>(reinterpret_cast<const float*>(rp + a), 0);
+      } else {
+        floatx4 v;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          int a = a0 + (16 * m + t) * (int)sizeof(T);
+          a -= a >= ring ? ring : 0;
+          v[t] = to_f(*reinterpret_cast<const T*>(rp + a));
+        }
+        return v;
+      }
+    };
+    auto mask_last = [&](floatx4& x) {  // lights past N in the last chunk: the next pixel's values
+#pragma unroll
+      for (int t = 0; t < 4; ++t) x[t] = t < nlast ? x[t] : 0.f;
+    };
+    floatx4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto mma = [&](floatx4 a, floatx4 x) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], x[t], acc[t], 0, 0, 0);
+    };
+    if constexpr (NCH > 0) {
+      floatx4 x[NCH];
+#pragma unroll
+      for (int m = 0; m < NCH; ++m)
+        if (m < nch) x[m] = rdx(m);
+#pragma unroll
+      for (int m = 0; m < NCH; ++m)  // (compile-time index: no dynamic indexing of the register array)
+        if (m == nch - 1 && (N & 15)) mask_last(x[m]);
+#pragma unroll
+      for (int m = 0; m < NCH; ++m)
+        if (m < nch) mma(areg[m], x[m]);
+    } else {
+      for (int m = 0; m < nch; ++m) {
+        floatx4 x = rdx(m);
+        if (m == nch - 1 && (N & 15)) mask_last(x);
+        mma(*reinterpret_cast<const floatx4*>(lpq + 16 * m), x);
+      }
+    }
+    const floatx4 d = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    store_group<K, LAYOUT>(rs, d, px0 + q, P, r);  // groups past P: every store dropped
+    // refill every KiB the groups 0..j freed
+    const int lim0 = (end + ring) >> 10;
+    const int lim = lim0 < dt ? lim0 : dt;
+    for (; issued < lim; ++issued) issue();
+    base += GBY;
+    base -= base >= ring ? ring : 0;
+    px0 += 16;
+    if (++gi == U) {
+      gi = 0;
+      ug += ust;
+      const int cg0 = cg;
+      while (ug >= nu) {
+        ug -= nu;
+        ++cg;
+      }
+      px0 = ug * U * 16;
+      if (cg != cg0 && cg < C)
+        rs = __builtin_amdgcn_make_buffer_rsrc(coef + (int64_t)cg * ocstride, (short)0, (int)(P * K * 4), 0x00020000);
+    }
+  }
+}
+
+// VALU streaming form (AUTO for k <= 9): the same units, interleaving and LDS ring as fit_pm_stream, but the
+// ring is consumed 64 pixels (4 groups of the stream) at a time with ONE PIXEL PER LANE: lane l reads its
+// pixel's row from the ring (ds_read_b128, 4 lights) and accumulates k coefficients with packed FMAs
+// (v_pk_fma_f32 over light pairs: acc_i.xy += I[n, n+1]·pinv[i][n, n+1], the weights wave-uniform in SGPRs,
+// read by scalar loads), so a pixel·light costs k/2 VALU lane-ops instead of the 16 MACs a 16x16x4 MFMA
+// spends on it whatever k (PTM-6: 10 of 16 matrix rows idle).  The lanes of a block may belong to different
+// units and channels: each lane keeps its own group cursor, and the coefficients leave by buffer stores
+// over the WHOLE coefficient array (per-lane 32-bit offsets; lanes past P or past the stream get an
+// out-of-range offset), so every block issues the same SB stores.
+template <int K, typename T, int LAYOUT, int ALIGN>
+__global__ void __launch_bounds__(256)
+fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
+               float* __restrict__ coef, int64_t ocstride, int C, int U, int nu, int64_t tu, int ring,
+               uint32_t coef_bytes) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int SB = LAYOUT == RTI_COEF_PIXEL_MAJOR ? (K % 2 == 0 ? K / 2 : K) : K;  // stores per block
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int W = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the operator in LDS as [N4/4][K][4] (zero padded): one broadcast ds_read_b128 gives pinv[i][n .. n+3]
+  const int N4 = (N + 3) & ~3;
+  float* __restrict__ lw = lds;
+  for (int idx = threadIdx.x; idx < N4 * K; idx += blockDim.x) {
+    const int nq = idx / (4 * K), rem = idx - nq * 4 * K, i = rem >> 2, n = 4 * nq + (rem & 3);
+    lw[idx] = n < N ? pinv[i * N + n] : 0.f;
+  }
+  __syncthreads();
+  char* __restrict__ rp = reinterpret_cast<char*>(lds + N4 * K) + wave * ring;
+  const int64_t gw = (int64_t)blockIdx.x * W + wave, GW = (int64_t)gridDim.x * W;
+  const int GBY = 16 * N * (int)sizeof(T);
+  const int64_t cbytes = P * N * (int64_t)sizeof(T);
+  const int slots = ring >> 10;
+  const int64_t nk = gw >= tu ? 0 : (tu - 1 - gw) / GW + 1;  // units w, w + GW, ...
+  if (nk == 0) return;
+  const int ust = (int)GW;
+  const int ng = (int)(nk * U);                  // groups of the stream
+  const int nb = (ng + 3) >> 2;                   // 64-pixel blocks
+  const int dt = (int)(nk * ((U * GBY) >> 10));  // DMAs of the stream
+  int cd = (int)(gw / nu), ud = (int)(gw - (int64_t)cd * nu);
+  const int UB = U * GBY, UKB = UB >> 10;
+  const char* gp;
+  const char* gend;
+  auto seek = [&]() {
+    const char* ch = reinterpret_cast<const char*>(I + cd * cstride);
+    gp = ch + (int64_t)ud * UB + 16 * lane;
+    gend = ch + cbytes - 16;
+  };
+  seek();
+  int left = UKB, wslot = 0;
+  auto issue = [&]() {
+    dma16(gp < gend ? gp : gend, reinterpret_cast<float*>(rp + wslot));
+    gp += 1024;
+    wslot += 1024;
+    wslot = wslot == ring ? 0 : wslot;
+    if (--left == 0) {
+      left = UKB;
+      ud += ust;
+      while (ud >= nu) {
+        ud -= nu;
+        ++cd;
+      }
+      if (cd < C) seek();
+    }
+  };
+  int issued = dt < slots ? dt : slots;
+  for (int d = 0; d < issued; ++d) issue();
+  // the lane's group cursor: stream group j = 4b + (lane >> 4) -> unit (lc, lu), group gi within it
+  int lc = (int)(gw / nu), lu = (int)(gw - (int64_t)lc * nu), gi = lane >> 4;  // (the prologue moved cd, ud)
+  {
+    while (gi >= U) {
+      gi -= U;
+      lu += ust;
+      while (lu >= nu) {
+        lu -= nu;
+        ++lc;
+      }
+    }
+  }
+  const int q = lane & 15;
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef, (short)0, (int)coef_bytes, 0x00020000);
+  int base = 0, gd = -1;
+  const int lrow = N * (int)sizeof(T) * lane;  // the lane's row inside a block
+  for (int b = 0; b < nb; ++b) {
+    const int gend_b = 4 * (b + 1) < ng ? 4 * (b + 1) : ng;
+    const int end = GBY * gend_b;
+    const int dn = ((end + 1023) >> 10) - 1;
+    // the refill after block g issues DMAs up to (GBY·min(4(g+1), ng) + ring)/1 KiB (prologue: ring/1 KiB)
+    while (((GBY * (4 * (gd + 1) < ng ? 4 * (gd + 1) : ng) + ring) >> 10) < dn + 1) ++gd;
+    const int nwait = (issued - 1 - dn) + SB * (b - 1 - gd);
+    wait_vm_dyn(nwait > 63 ? 63 : nwait);
+    int a0 = base + lrow;
+    a0 -= a0 >= ring ? ring : 0;
+    f2 acc[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) acc[i] = f2{0.f, 0.f};
+    float acc1[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) acc1[i] = 0.f;
+    int n = 0;
+    if constexpr (ALIGN == 4) {
+      // one step of 4 lights ahead: step n + 4's row values and weights are read (LDS: in order, counted
+      // waits) while step n's 2·K packed FMAs issue
+      auto rdx = [&](int nn) {
+        int a = a0 + nn * (int)sizeof(T);
+        a -= a >= ring ? ring : 0;
+        return lds4<4, T>(reinterpret_cast<const float*>(rp + a), 0);
+      };
+      auto step = [&](const floatx4& x, const floatx4 (&w)[K]) {
+        const f2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]};
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+          acc[i] = x01 * f2{w[i][0], w[i][1]} + acc[i];
+          acc[i] = x23 * f2{w[i][2], w[i][3]} + acc[i];
+        }
+      };
+      const int n4 = N & ~3;
+      if (n4 > 0) {
+        floatx4 x = rdx(0), w[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) w[i] = *reinterpret_cast<const floatx4*>(lw + 4 * i);
+        for (n = 4; n < n4; n += 4) {
+          const floatx4 xn = rdx(n);
+          floatx4 wn[K];
+#pragma unroll
+          for (int i = 0; i < K; ++i) wn[i] = *reinterpret_cast<const floatx4*>(lw + n * K + 4 * i);
+          __builtin_amdgcn_sched_barrier(0);
+          step(x, w);
+          x = xn;
+#pragma unroll
+          for (int i = 0; i < K; ++i) w[i] = wn[i];
+        }
+        step(x, w);
+      }
+    }
+    for (; n < N; ++n) {  // N % 4 (or every light when the rows are not 16-byte aligned)
+      int a = a0 + n * (int)sizeof(T);
+      a -= a >= ring ? ring : 0;
+      const float x = to_f(*reinterpret_cast<const T*>(rp + a));
+#pragma unroll
+      for (int i = 0; i < K; ++i) acc1[i] = fmaf(x, lw[(n >> 2) * 4 * K + 4 * i + (n & 3)], acc1[i]);
+    }
+    float c[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) c[i] = (acc[i][0] + acc[i][1]) + acc1[i];
+    // stores: pixel px of channel lc; lanes past the stream or past P drop theirs
+    const int px = (lu * U + gi) * 16 + q;
+    const bool ok = 4 * b + (lane >> 4) < ng && px < P;
+    const uint32_t cb = (uint32_t)((int64_t)lc * ocstride * 4);
+    if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0) {
+#pragma unroll
+      for (int i = 0; i < K; i += 2) {
+        const uint32_t off = ok ? cb + (uint32_t)((px * K + i) * 4) : PM_OOB_ALL;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(intx2, f2{c[i], c[i + 1]}), rs, off, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const int64_t e = LAYOUT == RTI_COEF_PIXEL_MAJOR ? (int64_t)px * K + i : (int64_t)i * P + px;
+        const uint32_t off = ok ? cb + (uint32_t)(e * 4) : PM_OOB_ALL;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(c[i]), rs, off, 0, 0);
+      }
+    }
+    // refill every KiB the blocks 0..b freed
+    const int lim0 = (end + ring) >> 10;
+    const int lim = lim0 < dt ? lim0 : dt;
+    for (; issued < lim; ++issued) issue();
+    base += 4 * GBY;
+    base -= base >= ring ? ring : 0;
+    gi += 4;  // the lane's next group: 4 further along the stream
+    while (gi >= U) {
+      gi -= U;
+      lu += ust;
+      while (lu >= nu) {
+        lu -= nu;
+        ++lc;
+      }
+    }
+  }
+}
+
+// one lane per pixel: the fallback for every shape the DMA kernel does not take
+template <int K, typename T, int LAYOUT>
+__global__ void __launch_bounds__(256)
+fit_pm_lane(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P, int64_t pstride,
+            int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const T* __restrict__ row = I + (int64_t)blockIdx.y * cstride + p * pstride;
+  float acc[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) acc[i] = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const float x = (float)row[n];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+      if (i < k) acc[i] = fmaf(pinv[i * N + n], x, acc[i]);  // wave-uniform: s_load
+  }
+  float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
+#pragma unroll
+  for (int i = 0; i < K; ++i)
+    if (i < k) dst[LAYOUT == RTI_COEF_PIXEL_MAJOR ? p * k + i : (int64_t)i * P + p] = acc[i];
+}
+
+struct PmArgs {
+  const float* pinv;
+  int k, N;
+  const void* I;
+  int64_t P;
+  int C;
+  int64_t ps, cs;
+  float* coef;
+  int layout;
+  int64_t ocs;
+  hipStream_t stream;
+};
+
+// LDS plan of the DMA kernel: G groups of 16 pixels per block, W waves per workgroup
+struct PmPlan {
+  int G = 0, W = 0, slot = 0;
+  size_t lds = 0;
+};
+
+PmPlan pm_plan(int N, size_t es, int g_req, int w_req) {
+  const size_t op = (size_t)16 * ((N + 15) & ~15) * sizeof(float);
+  for (int G : {4, 2, 1}) {
+    if (g_req && G != g_req) continue;
+    // floats: whole KiB for the DMAs + 16 floats the masked tail chunk may read past the block
+    const int slot = (int)((((int64_t)16 * G * N * es + 1023) >> 10) << 8) + 16;
+    const size_t per_wave = (size_t)2 * slot * sizeof(float);
+    if (op + per_wave > (size_t)PM_LDS) continue;
+    int W = (int)((PM_LDS - op) / per_wave);
+    W = W > 8 ? 8 : W;
+    if (w_req) {
+      if (w_req > W) continue;
+      W = w_req;
+    }
+    // AUTO: the widest block that still leaves >= 4 waves per CU, else the most waves
+    if (!g_req && !w_req && W < 4 && G > 1) continue;
+    PmPlan pl;
+    pl.G = G;
+    pl.W = W;
+    pl.slot = slot;
+    pl.lds = op + (size_t)W * per_wave;
+    return pl;
+  }
+  return PmPlan();
+}
+
+template <int G, int K, typename T, int LAYOUT, int ALIGN>
+int launch_dma_t(const PmArgs& a, const PmPlan& pl) {
+  auto kern = fit_pm_dma<G, K, T, LAYOUT, ALIGN>;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)pl.lds) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
+  const int64_t nblk = (a.P + 16 * G - 1) / (16 * G), units = nblk * a.C;
+  const int64_t wgs_needed = (units + pl.W - 1) / pl.W;
+  const int64_t cus = device_cus();
+  const unsigned grid = (unsigned)(wgs_needed < cus ? wgs_needed : cus);  // one workgroup per CU (LDS-bound)
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * pl.W), pl.lds, a.stream, a.pinv, a.N, static_cast<const T*>(a.I),
+                     a.P, a.cs, a.coef, a.ocs, nblk, units, pl.slot);
+  return RTI_OK;
+}
+
+template <int G, int K, typename T, int LAYOUT>
+int launch_dma_a(const PmArgs& a, const PmPlan& pl) {
+  if (a.N % 4 == 0) return launch_dma_t<G, K, T, LAYOUT, 4>(a, pl);
+  if (a.N % 2 == 0) return launch_dma_t<G, K, T, LAYOUT, 2>(a, pl);
+  return launch_dma_t<G, K, T, LAYOUT, 1>(a, pl);
+}
+
+template <int K, typename T, int LAYOUT>
+int launch_dma_g(const PmArgs& a, const PmPlan& pl) {
+  switch (pl.G) {
+    case 4: return launch_dma_a<4, K, T, LAYOUT>(a, pl);
+    case 2: return launch_dma_a<2, K, T, LAYOUT>(a, pl);
+    default: return launch_dma_a<1, K, T, LAYOUT>(a, pl);
+  }
+}
+
+template <int K, typename T>
+int launch_dma_l(const PmArgs& a, const PmPlan& pl) {
+  return a.layout == RTI_COEF_PLANAR ? launch_dma_g<K, T, RTI_COEF_PLANAR>(a, pl)
+                                     : launch_dma_g<K, T, RTI_COEF_PIXEL_MAJOR>(a, pl);
+}
+
+template <typename T>
+int launch_dma(const PmArgs& a, const PmPlan& pl) {
+  switch (a.k) {
+    case 6: return launch_dma_l<6, T>(a, pl);
+    case 9: return launch_dma_l<9, T>(a, pl);
+    case 16: return launch_dma_l<16, T>(a, pl);
+    default: return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: k=%d", a.k);
+  }
+}
+
+// streaming plan: W waves per workgroup (one workgroup per CU), a ring of whole KiB per wave that holds at
+// least one group + 1 KiB.  AUTO takes the most waves that fit: the wave's issue rate, not the bytes in
+// flight, bounds the stream (c3 4K×100: 8 waves 0.665 ms with 19-KiB rings, 4 waves 0.82, 2 waves 1.57
+// with 76-KiB rings; c4 4K RGB×200: 8 waves 3.80 ms, 4 waves 4.15-4.63; profiles/r04_pm_sweep.log)
+struct StreamPlan {
+  int W = 0, ring = 0, contig = 0, unit = 1;
+  size_t lds = 0;
+};
+
+StreamPlan stream_plan(int N, size_t es, int w_req, int u_req) {
+  const size_t op = (size_t)16 * ((N + 15) & ~15) * sizeof(float);
+  const int64_t gby = (int64_t)16 * N * es;
+  for (int W : {8, 6, 4, 3, 2, 1}) {
+    if (w_req && W != w_req) continue;
+    if (op >= (size_t)PM_LDS) break;
+    const int ring = (int)(((PM_LDS - op) / W) >> 10 << 10);
+    if (ring < gby + 1024) continue;
+    StreamPlan pl;
+    pl.W = W;
+    pl.ring = ring;
+    pl.lds = op + (size_t)W * ring;
+    pl.unit = u_req > 0 ? u_req : 1;
+    return pl;
+  }
+  return StreamPlan();
+}
+
+template <int K, typename T, int LAYOUT, int ALIGN, int NCH>
+int launch_stream_t(const PmArgs& a, const StreamPlan& pl) {
+  auto kern = fit_pm_stream<K, T, LAYOUT, ALIGN, NCH>;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)pl.lds) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
+  const int64_t cus = device_cus();
+  int g = 16, nn = a.N;  // U = (16 / gcd(N, 16)) · unit: a whole number of KiB (4-byte values)
+  while (g > 1 && nn % g) g >>= 1;
+  const int U = 16 / g * pl.unit;
+  const int64_t nu = (a.P + 16 * U - 1) / (16 * U), tu = nu * a.C;
+  if (nu >= ((int64_t)1 << 31) / (16 * U)) return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: P too large");
+  const int64_t wgs = (tu + pl.W - 1) / pl.W;
+  const unsigned grid = (unsigned)(wgs < cus ? wgs : cus);  // one workgroup per CU (LDS-bound)
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * pl.W), pl.lds, a.stream, a.pinv, a.N, static_cast<const T*>(a.I),
+                     a.P, a.cs, a.coef, a.ocs, a.C, U, (int)nu, tu, pl.ring, pl.contig);
+  return RTI_OK;
+}
+
+template <int K, typename T, int LAYOUT, int ALIGN>
+int launch_stream_n(const PmArgs& a, const StreamPlan& pl) {
+  const int nch = (a.N + 15) >> 4;
+  if (nch <= 4) return launch_stream_t<K, T, LAYOUT, ALIGN, 4>(a, pl);
+  if (nch <= 8) return launch_stream_t<K, T, LAYOUT, ALIGN, 8>(a, pl);
+  if (nch <= 16) return launch_stream_t<K, T, LAYOUT, ALIGN, 16>(a, pl);
+  return launch_stream_t<K, T, LAYOUT, ALIGN, 0>(a, pl);
+}
+
+template <int K, typename T, int LAYOUT>
+int launch_stream_a(const PmArgs& a, const StreamPlan& pl) {
+  if (a.N % 4 == 0) return launch_stream_n<K, T, LAYOUT, 4>(a, pl);
+  return launch_stream_n<K, T, LAYOUT, 1>(a, pl);
+}
+
+template <typename T>
+int launch_stream(const PmArgs& a, const StreamPlan& pl) {
+  const bool planar = a.layout == RTI_COEF_PLANAR;
+  switch (a.k) {
+    case 6: return planar ? launch_stream_a<6, T, RTI_COEF_PLANAR>(a, pl) : launch_stream_a<6, T, RTI_COEF_PIXEL_MAJOR>(a, pl);
+    case 9: return planar ? launch_stream_a<9, T, RTI_COEF_PLANAR>(a, pl) : launch_stream_a<9, T, RTI_COEF_PIXEL_MAJOR>(a, pl);
+    case 16: return planar ? launch_stream_a<16, T, RTI_COEF_PLANAR>(a, pl) : launch_stream_a<16, T, RTI_COEF_PIXEL_MAJOR>(a, pl);
+    default: return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: k=%d", a.k);
+  }
+}
+
+// VALU stream (k <= 9): one workgroup of W waves per CU (W <= 4, one per SIMD), a ring per wave that holds a
+// 64-pixel block (4 groups) + 1 KiB; AUTO takes the most waves that fit (4 up to N = 150 for 4-byte values)
+struct VPlan {
+  int W = 0, ring = 0;
+  size_t lds = 0;
+};
+
+VPlan vstream_plan(int k, int N, size_t es, int w_req) {
+  if (k > 9) return VPlan();
+  const int64_t need = (int64_t)4 * 16 * N * es + 1024;
+  const size_t op = (size_t)((N + 3) & ~3) * (k <= 6 ? 6 : 9) * sizeof(float);
+  for (int W : {4, 3, 2, 1}) {
+    if (w_req && W != w_req) continue;
+    const int ring = (int)(((PM_LDS - op) / W) >> 10 << 10);
+    if (ring < need) continue;
+    VPlan pl;
+    pl.W = W;
+    pl.ring = ring;
+    pl.lds = op + (size_t)W * ring;
+    return pl;
+  }
+  return VPlan();
+}
+
+template <int K, typename T, int LAYOUT, int ALIGN>
+int launch_vstream_t(const PmArgs& a, const VPlan& pl) {
+  auto kern = fit_pm_vstream<K, T, LAYOUT, ALIGN>;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)pl.lds) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
+  const int64_t cus = device_cus();
+  int g = 16, nn = a.N;  // U = 16 / gcd(N, 16): units of a whole number of KiB
+  while (g > 1 && nn % g) g >>= 1;
+  const int U = 16 / g;
+  const int64_t nu = (a.P + 16 * U - 1) / (16 * U), tu = nu * a.C;
+  if (nu >= ((int64_t)1 << 31) / (16 * U)) return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: P too large");
+  const int64_t wgs = (tu + pl.W - 1) / pl.W;
+  const unsigned grid = (unsigned)(wgs < cus ? wgs : cus);
+  const uint64_t cb = (uint64_t)a.ocs * (a.C - 1) * 4 + (uint64_t)a.P * K * 4;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * pl.W), pl.lds, a.stream, a.pinv, a.N, static_cast<const T*>(a.I),
+                     a.P, a.cs, a.coef, a.ocs, a.C, U, (int)nu, tu, pl.ring, (uint32_t)cb);
+  return RTI_OK;
+}
+
+template <int K, typename T>
+int launch_vstream_k(const PmArgs& a, const VPlan& pl) {
+  const bool planar = a.layout == RTI_COEF_PLANAR;
+  if (a.N % 4 == 0)
+    return planar ? launch_vstream_t<K, T, RTI_COEF_PLANAR, 4>(a, pl) : launch_vstream_t<K, T, RTI_COEF_PIXEL_MAJOR, 4>(a, pl);
+  return planar ? launch_vstream_t<K, T, RTI_COEF_PLANAR, 1>(a, pl) : launch_vstream_t<K, T, RTI_COEF_PIXEL_MAJOR, 1>(a, pl);
+}
+
+template <typename T>
+int launch_vstream(const PmArgs& a, const VPlan& pl) {
+  return a.k == 6 ? launch_vstream_k<6, T>(a, pl) : launch_vstream_k<9, T>(a, pl);
+}
+
+// the whole coefficient array must be addressable by 32-bit buffer offsets
+static bool vstream_coef_ok(const PmArgs& a) {
+  return (uint64_t)a.ocs * (a.C - 1) * 4 + (uint64_t)a.P * a.k * 4 < 0xFFFFFFF0ull;
+}
+
+template <int K, typename T>
+void launch_lane_t(const PmArgs& a) {
+  const dim3 grid(grid_1d(a.P, 256), a.C);
+  if (a.layout == RTI_COEF_PLANAR)
+    hipLaunchKernelGGL((fit_pm_lane<K, T, RTI_COEF_PLANAR>), grid, dim3(256), 0, a.stream, a.pinv, a.k, a.N,
+                       static_cast<const T*>(a.I), a.P, a.ps, a.cs, a.coef, a.ocs);
+  else
+    hipLaunchKernelGGL((fit_pm_lane<K, T, RTI_COEF_PIXEL_MAJOR>), grid, dim3(256), 0, a.stream, a.pinv, a.k, a.N,
+                       static_cast<const T*>(a.I), a.P, a.ps, a.cs, a.coef, a.ocs);
+}
+
+template <typename T>
+void launch_lane(const PmArgs& a) {
+  if (a.k <= 6)
+    launch_lane_t<6, T>(a);
+  else if (a.k <= 9)
+    launch_lane_t<9, T>(a);
+  else
+    launch_lane_t<16, T>(a);
+}
+
+}  // namespace
+}  // namespace rti
+
+using namespace rti;
+
+// the shapes the DMA/MFMA kernels take (both forms)
+static bool pm_dma_shape(int k, int N, int in_dtype, int64_t P, int C, int64_t ps, int64_t cs) {
+  if (k != 6 && k != 9 && k != 16) return false;
+  if (in_dtype != RTI_F32 && in_dtype != RTI_I32) return false;
+  return ps == N && (P * N) % 4 == 0 && (C <= 1 || cs % 4 == 0) && P * (int64_t)k * 4 < ((int64_t)1 << 31);
+}
+
+extern "C" int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int C, int64_t pixel_stride,
+                                      int64_t channel_stride, int kernel) {
+  const int64_t ps = pixel_stride ? pixel_stride : N;
+  const int64_t cs = channel_stride ? channel_stride : P * ps;
+  if (!pm_dma_shape(k, N, in_dtype, P, C, ps, cs) || (kernel & 0xff) == RTI_KERNEL_VALU) return 0;
+  const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  if ((kernel & 0xff) == RTI_KERNEL_AUTO) {
+    const VPlan vp = vstream_plan(k, N, 4, w_req);
+    if (vp.W && (int64_t)C * P * k * 4 < 0xFFFFFFF0ll)
+      return -(int)(((vp.ring >> 10) * 1000 + vp.W) + 100000000);  // VALU stream: −(1e8 + ring KiB·1000 + W)
+  }
+  if ((kernel & 0xff) != RTI_KERNEL_TILE) {
+    const StreamPlan sp = stream_plan(N, 4, w_req, c_req);
+    if (sp.W) return (sp.ring >> 10) * 1000 + sp.W;  // KiB of ring per wave · 1000 + waves per workgroup
+  }
+  // the double-buffered block form (kernel TILE, or N < 16)
+  const PmPlan pl = pm_plan(N, 4, (kernel & 0xff) == RTI_KERNEL_TILE ? c_req : 0, w_req);
+  return pl.G ? -(16 * pl.G * 1000 + pl.W) : 0;  // −(pixels per block · 1000 + waves per workgroup)
+}
+
+extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
+                                 int64_t pixel_stride, int64_t channel_stride, float* coef, int coef_layout,
+                                 int64_t coef_channel_stride, int kernel, rti_stream_t stream) {
+  if (!pinv || !I || !coef) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: null pointer");
+  if (N <= 0 || P <= 0 || C <= 0 || C > 65535) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: bad N/P/C");
+  if (k < 1 || k > 16) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: k=%d outside 1..16", k);
+  if (N < k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: N=%d < k=%d", N, k);
+  if (in_dtype != RTI_F32 && in_dtype != RTI_U8 && in_dtype != RTI_I32)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: input dtype %d", in_dtype);
+  if (coef_layout != RTI_COEF_PIXEL_MAJOR && coef_layout != RTI_COEF_PLANAR)
+    return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: coef layout %d", coef_layout);
+  PmArgs a;
+  a.pinv = pinv;
+  a.k = k;
+  a.N = N;
+  a.I = I;
+  a.P = P;
+  a.C = C;
+  a.ps = pixel_stride ? pixel_stride : N;
+  a.cs = channel_stride ? channel_stride : P * a.ps;
+  a.coef = coef;
+  a.layout = coef_layout;
+  a.ocs = coef_channel_stride ? coef_channel_stride : P * k;
+  a.stream = (hipStream_t)stream;
+  if (a.ps < N) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: pixel_stride < N");
+  if (C > 1 && a.cs < P * a.ps) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: channel_stride");
+  if (C > 1 && a.ocs < P * k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: coef_channel_stride");
+  note_launches(1);
+  const int sel = kernel & 0xff;
+  const size_t es = in_dtype == RTI_U8 ? 1 : 4;
+  const bool dma_ok = sel != RTI_KERNEL_VALU &&
+                      rti_fit_shared_pm_plan(k, N, in_dtype, P, C, a.ps, a.cs, kernel) != 0 &&
+                      aligned_to(I, 16) && aligned_to(coef, 16) && a.ocs % 4 == 0;
+  const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  if (dma_ok && sel == RTI_KERNEL_AUTO) {  // k <= 9: one pixel per lane, packed FMAs
+    const VPlan vp = vstream_plan(k, N, es, w_req);
+    if (vp.W && vstream_coef_ok(a)) {
+      const int st = in_dtype == RTI_F32 ? launch_vstream<float>(a, vp) : launch_vstream<int32_t>(a, vp);
+      return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
+    }
+  }
+  if (dma_ok) {
+    StreamPlan sp;
+    if (sel != RTI_KERNEL_TILE) sp = stream_plan(N, es, w_req, c_req);
+    int st;
+    if (sp.W) {  // AUTO / MFMA: the streaming ring
+      sp.contig = (kernel & RTI_KERNEL_ROTATE) != 0;  // measurement: each wave one contiguous run of units
+      st = in_dtype == RTI_F32 ? launch_stream<float>(a, sp) : launch_stream<int32_t>(a, sp);
+    } else {  // the double-buffered block form (kernel TILE, or N < 16)
+      const PmPlan pl = pm_plan(N, es, sel == RTI_KERNEL_TILE ? c_req : 0, w_req);
+      st = in_dtype == RTI_F32 ? launch_dma<float>(a, pl) : launch_dma<int32_t>(a, pl);
+    }
+    return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
+  }
+  if (sel == RTI_KERNEL_MFMA || sel == RTI_KERNEL_TILE)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: the DMA/MFMA kernels do not take this shape");
+  switch (in_dtype) {
+    case RTI_F32: launch_lane<float>(a); break;
+    case RTI_I32: launch_lane<int32_t>(a); break;
+    default: launch_lane<uint8_t>(a); break;
+  }
+  return check_launch("rti_fit_shared_pm");
+}

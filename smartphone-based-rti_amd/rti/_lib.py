@@ -84,6 +84,9 @@ SIGNATURES = {
     "rti_lsq_factors": (_c_int, [_c_int, _c_float_p, _c_float_p, _c_int, _c_double, _c_double_p, _c_double_p]),
     "rti_fit_shared": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_int, _c_i64, _c_int, _c_i64, _c_i64,
                                 _c_void_p, _c_int, _c_i64, _c_int, _c_void_p]),
+    "rti_fit_shared_pm": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_int, _c_i64, _c_int, _c_i64, _c_i64,
+                                   _c_void_p, _c_int, _c_i64, _c_int, _c_void_p]),
+    "rti_fit_shared_pm_plan": (_c_int, [_c_int, _c_int, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int]),
     "rti_q8_operator_bytes": (_c_i64, [_c_int, _c_int]),
     "rti_q8_operator": (_c_int, [_c_double_p, _c_int, _c_int, _c_void_p]),
     "rti_fit_shared_q8_max_lights": (_c_int, []),

@@ -177,6 +177,45 @@ def fit_q8_into(op_dev, I, coef, *, k, layout="pixel", flags=0):
     return coef
 
 
+def _fit_shared_pixel_major(I, lu, lv, b, k, rcond, cl, kernel, given_pixel_major):
+    """rti.fit(mode="shared") on a pixel-major stack: ``rti_fit_shared_pm`` on the tensor's own memory."""
+    if given_pixel_major:
+        if I.dim() == 2:
+            spatial, C = (I.shape[0],), 1
+        elif I.dim() == 3:
+            spatial, C = tuple(I.shape[:2]), 1
+        elif I.dim() == 4:
+            spatial, C = tuple(I.shape[1:3]), I.shape[0]
+        else:
+            raise ValueError("pixel-major I must be [P, N], [H, W, N] or [C, H, W, N]")
+        N = I.shape[-1]
+        v = I if I.stride(-1) == 1 else I.contiguous()
+        if v.dim() == 3 and C == 1:
+            v = v.reshape(-1, N)
+        v = v.reshape(C, -1, N)
+        lead4 = I.dim() == 4
+    else:
+        v = _pixel_major_of(I)
+        C, N = v.shape[0], v.shape[2]
+        spatial = tuple(I.shape[-2:]) if I.dim() >= 3 else (I.shape[-1],)
+        lead4 = I.dim() == 4
+    P = v.shape[1]
+    if N < k:
+        raise ValueError(f"shapes not aligned: {N} lights < {k} basis terms (analysis.py:298)")
+    pv = pinv(lu, lv, b, rcond)
+    if pv.shape[1] != N:
+        raise ValueError(f"{pv.shape[1]} light directions for {N} intensity values per pixel")
+    if I.dtype not in _IN_DTYPES:
+        raise ValueError(f"I dtype {I.dtype} unsupported (float32, uint8 or int32)")
+    coef = torch.empty((C, P, k) if cl == L.RTI_COEF_PIXEL_MAJOR else (C, k, P), dtype=torch.float32,
+                       device=I.device)
+    kern = kernel if kernel in ("auto", "mfma", "valu") else "auto"
+    fit_shared_pm_into(torch.as_tensor(pv.astype(np.float32), device=I.device), v, coef, k=k, layout=cl,
+                       kernel=kern)
+    out = coef.reshape((C,) + spatial + (k,)) if cl == L.RTI_COEF_PIXEL_MAJOR else coef.reshape((C, k) + spatial)
+    return out if lead4 else out[0]
+
+
 def basis_eval(lu, lv, basis="ptm"):
     """Host fp64 basis values [E, k] at (lu, lv)."""
     lu = np.ascontiguousarray(np.asarray(lu, np.float64).ravel())
@@ -227,14 +266,62 @@ def fit_shared_into(pinv_dev, I, coef, *, k, layout="pixel", kernel="auto", nont
     return coef
 
 
+def fit_shared_pm_into(pinv_dev, I, coef, *, k, layout="pixel", kernel="auto", flags=0):
+    """Launch ``rti_fit_shared_pm`` (pixel-major stacks, the reference's (R, R, N) layout,
+    analysis.py:217-219) on preallocated tensors: pinv_dev CUDA fp32 [k, N]; I CUDA [P, N] or [C, P, N]
+    with unit light stride (any pixel / channel stride, e.g. a view of [H, W, N]); coef as
+    fit_shared_into."""
+    I3 = I if I.dim() == 3 else I.unsqueeze(0)
+    C, P, N = I3.shape
+    if I3.stride(2) != 1 and N > 1:
+        raise ValueError("pixel-major stack needs unit light stride (I[..., p, n] with n contiguous)")
+    ps = I3.stride(1) if P > 1 else N
+    cs = I3.stride(0) if C > 1 else P * ps
+    kern = _KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+    kern = (kern & 0xff) | int(flags)
+    st = L.lib().rti_fit_shared_pm(_vp(pinv_dev), k, N, _vp(I3), _IN_DTYPES[I.dtype], P, C, ps, cs, _vp(coef),
+                                   _layout_id(layout), P * k, kern, _stream_of(I))
+    L.check(st, "rti_fit_shared_pm")
+    return coef
+
+
+def _pixel_major_of(I):
+    """A light-major-shaped stack ([N, P], [N, H, W], [C, N, H, W]) that is a view of a pixel-major one
+    (I.permute of the reference's [H, W, N]) -> the same data as [C, P, N] with unit light stride, else None."""
+    if I.dim() < 2 or I.dim() > 4 or I.stride(1 if I.dim() == 4 else 0) != 1:
+        return None  # the light dimension must be the unit-stride one
+    if I.dim() == 2:
+        v = I.t().unsqueeze(0)
+    elif I.dim() == 3:
+        N, H, W = I.shape
+        if I.stride(1) != W * I.stride(2):
+            return None
+        v = I.permute(1, 2, 0).reshape(1, H * W, N) if H * W > 0 else None
+    else:
+        C, N, H, W = I.shape
+        if I.stride(2) != W * I.stride(3):
+            return None
+        v = I.permute(0, 2, 3, 1).reshape(C, H * W, N)
+    if v is None or v.data_ptr() != I.data_ptr() or v.stride(2) != 1 or v.shape[2] < 2:
+        return None  # reshape copied: not a view
+    return v
+
+
 def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=None, origin=(0.0, 0.0),
-        layout="pixel", kernel="auto", coef_dtype=torch.float32, nontemporal=False):
+        layout="pixel", kernel="auto", coef_dtype=torch.float32, nontemporal=False, stack="auto"):
     """Fit per-pixel reflectance coefficients on the GPU.
 
     mode="shared" (the north_star path; directional lights, one (lu, lv) per light):
-        I: CUDA tensor [N, H, W], [N, P] or [C, N, H, W] (light-major), fp32/u8/int32.
+        I: CUDA tensor [N, H, W], [N, P] or [C, N, H, W] (light-major), fp32/u8/int32;
+        with stack="pixel" the reference's own pixel-major layout instead, [H, W, N], [P, N] or
+        [C, H, W, N] (analysis.py:217-219), fitted in place by ``rti_fit_shared_pm`` (no transpose).
+        stack="auto" also routes a light-major-shaped VIEW of a pixel-major stack (``Ipm.permute(2, 0, 1)``)
+        to that kernel instead of copying it.
         lu, lv: N light directions (host or device).  Returns fp32 coefficients
         [.., H, W, k] (layout="pixel") or [.., k, H, W] (layout="planar").
+        uint8 light-major stacks run the split-fp16 MFMA kernel under kernel="auto" (``rti_fit_shared_h16``:
+        the operator carried to 22 significant bits, fp32 sums; within ≈1e-6 of max|c| of the fp32 stream
+        that ``fit_shared_into`` / ``torch.ops.rti.fit_shared`` run on the same stack).
     mode="perpixel" (the reference's geometry, PTM only):
         either cams=[N, 3] camera positions with I light-major [N, H, W]
         (directions generated in-kernel, pixel (x, y) at origin + (x, y, 0)),
@@ -248,6 +335,10 @@ def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=Non
             raise ValueError("shared mode needs lu and lv (one direction per light)")
         b = basis_id(basis)
         k = basis_terms(b)
+        if stack not in ("auto", "light", "pixel"):
+            raise ValueError(f"unknown stack layout {stack!r} (expected 'auto', 'light' or 'pixel')")
+        if stack == "pixel" or (stack == "auto" and not I.is_contiguous() and _pixel_major_of(I) is not None):
+            return _fit_shared_pixel_major(I, lu, lv, b, k, rcond, cl, kernel, stack == "pixel")
         lead = I.shape[:-2] if I.dim() >= 3 else I.shape[:-1]
         if I.dim() == 2:
             N, P = I.shape

@@ -134,9 +134,11 @@ def test_custom_op_matches_api(cuda):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("kernel", KERNELS)
-def test_full_size_4k_n100_properties(cuda, kernel):
-    """BASELINE configs[2] size (3840x2160, N=100): sampled fp64 parity, exact recovery, linearity."""
+@pytest.mark.parametrize("kernel,layout", [(k, "planar") for k in KERNELS] + [("auto", "pixel")])
+def test_full_size_4k_n100_properties(cuda, kernel, layout):
+    """BASELINE configs[2] size (3840x2160, N=100): sampled fp64 parity, exact recovery, linearity.
+    ("auto", "pixel") is bench.py's headline path exactly: fit_shared_valu as 4 launch generations with
+    LDS-staged pixel-major stores."""
     H, W, N = 2160, 3840, 100
     lu, lv = o.synth_dirs(N, 2)
     g = torch.Generator(device=cuda).manual_seed(0)
@@ -149,7 +151,13 @@ def test_full_size_4k_n100_properties(cuda, kernel):
         for j in range(6):
             row.add_(a_true[j], alpha=float(B[n, j]))
         I[n] = row
-    coef = rti.fit(I.reshape(N, H, W), lu, lv, kernel=kernel, layout="planar").reshape(6, -1)
+    def fit6(stack):  # [6, P] whatever the layout
+        c = rti.fit(stack.reshape(N, H, W), lu, lv, kernel=kernel, layout=layout)
+        return c.reshape(6, -1) if layout == "planar" else c.reshape(-1, 6).T
+
+    coef = fit6(I)
+    if kernel == "auto":
+        assert int(rti._lib.lib().rti_last_launch_count()) == 4  # the bench's 4 launch generations
     # sampled pixels against the fp64 oracle on the same fp32 stack
     idx = torch.randint(0, H * W, (4096,), generator=g, device=cuda)
     ref = o.fit_shared(I[:, idx].cpu().numpy(), o.pinv_shared("ptm", lu, lv))
@@ -159,7 +167,7 @@ def test_full_size_4k_n100_properties(cuda, kernel):
     scale = a_true.abs().amax(0).clamp_min(1.0)
     assert float(((coef - a_true).abs() / scale).max()) < 1e-4
     # linearity: fit(2I + 3) = 2 fit(I) + 3 pinv·1
-    coef2 = rti.fit((2 * I + 3).reshape(N, H, W), lu, lv, kernel=kernel, layout="planar").reshape(6, -1)
+    coef2 = fit6(2 * I + 3)
     c3 = torch.as_tensor(o.pinv_shared("ptm", lu, lv).sum(1) * 3, device=cuda, dtype=torch.float32)[:, None]
     assert float(((coef2 - 2 * coef - c3).abs() / (2 * scale)).max()) < 1e-4
 

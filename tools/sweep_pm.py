@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Pixel-major shared fit (rti_fit_shared_pm) variants next to the light-major AUTO fit of the same
+values, interleaved in ONE process (HIP events per launch, median of --rounds):
+streaming ring at W waves per workgroup ("mfma", AUTO's form) and the double-buffered block form
+("tile", G 16-pixel groups per block).
+
+  python tools/sweep_pm.py --config c3|c4|c2 [--rounds 20] [--waves 2,3,4,6,8] [--blocks 1,2,4]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "smartphone-based-rti_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import rti  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
+    ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--waves", default="2,3,4,6,8")
+    ap.add_argument("--blocks", default="1,2")
+    ap.add_argument("--in-dtype", default="f32", choices=["f32", "i32"])
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    L = rti._lib
+    _, H, W, N, C, basis, _ = bench.CONFIGS[args.config]
+    k = rti.basis_terms(basis)
+    P = H * W
+    lu, lv = bench.synth_dirs(N, 2)
+    I = bench.synth_stack(H, W, N, C, basis, lu, lv, 1000, dev)
+    if args.in_dtype == "i32":
+        I = I.to(torch.int32)
+    Ipm = I.transpose(1, 2).contiguous()  # [C, P, N]
+    pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=dev)
+    coef = torch.empty((C, P, k), device=dev)
+    ref = torch.empty((C, P, k), device=dev)
+    variants = [("light_major_auto", lambda: rti.fit_shared_into(pv, I, ref, k=k, layout="pixel", kernel="auto"))]
+    for w in [int(x) for x in args.waves.split(",") if x]:
+        fl = w << L.RTI_KERNEL_TILE_WAVES_SHIFT
+        plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl | L.RTI_KERNEL_MFMA)
+        if plan:
+            variants.append((f"pm_stream_w{w}_ring{plan // 1000}K",
+                             lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="mfma", flags=fl)))
+        if plan and w == 8:
+            for u in (2, 4):
+                flu = fl | (u << L.RTI_KERNEL_CHUNKS_SHIFT)
+                variants.append((f"pm_stream_w{w}_unit{u}",
+                                 lambda flu=flu: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="mfma", flags=flu)))
+            flc = fl | L.RTI_KERNEL_ROTATE
+            variants.append((f"pm_stream_w{w}_contiguous",
+                             lambda flc=flc: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="mfma", flags=flc)))
+    for g in [int(x) for x in args.blocks.split(",") if x]:
+        fl = g << L.RTI_KERNEL_CHUNKS_SHIFT
+        plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl | L.RTI_KERNEL_TILE)
+        if plan:
+            variants.append((f"pm_block_{abs(plan) // 1000}px_w{abs(plan) % 1000}",
+                             lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="tile", flags=fl)))
+    for w in (4, 3, 2):
+        fl = w << L.RTI_KERNEL_TILE_WAVES_SHIFT
+        plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
+        if plan <= -100000000:
+            variants.append((f"pm_valu_w{w}_ring{(-plan - 100000000) // 1000}K",
+                             lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
+    variants.append(("pm_auto", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto")))
+    agree = {}
+    for name, fn in variants:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        if name != "light_major_auto":
+            scale = ref.abs().amax(-1, keepdim=True).clamp_min(1e-30)
+            agree[name] = float(((coef - ref).abs() / scale).max())
+            coef.fill_(float("nan"))
+    stream = torch.cuda.current_stream(dev)
+    times = {name: [] for name, _ in variants}
+    for _ in range(args.rounds):
+        for name, fn in variants:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fn()
+            b.record(stream)
+            times[name].append((a, b))
+        torch.cuda.synchronize()
+    alg = 4.0 * P * N * C + 4.0 * P * k * C
+    res = {}
+    for name, _ in variants:
+        ms = float(np.median([a.elapsed_time(b) for a, b in times[name]]))
+        gbs = alg / (ms * 1e-3) / 1e9
+        res[name] = {"median_ms": ms, "GBps": gbs, "frac_8TBps": gbs / 8000.0, "max_rel_vs_light": agree.get(name)}
+        print(f"{name:28s} {ms:.4f} ms  {gbs:.0f} GB/s ({gbs / 8000:.3f} of 8 TB/s)"
+              + (f"  rel {agree[name]:.1e}" if name in agree else ""), flush=True)
+    print(json.dumps({"config": args.config, "alg_bytes": alg, "results": res}))
+
+
+if __name__ == "__main__":
+    main()
