@@ -380,7 +380,9 @@ class FitWorkload(Workload):
                "coef_layout": self.args.layout, "kernel": self.u8_kernel or self.args.kernel,
                "intensity_dtype": self.args.in_dtype, "stack_layout": self.stack}
         if self.stack == "pixel":
-            cfg["pm_plan"] = {"pixels_per_block": self.pm_plan // 1000, "waves_per_cu": self.pm_plan % 1000} \
+            form = {1: "valu stream (one pixel per lane, packed FMA)", 2: "mfma stream", 3: "mfma block"}
+            cfg["pm_plan"] = {"form": form.get(self.pm_plan // 100000000), "waves_per_cu": self.pm_plan % 1000,
+                              "kib_ring_or_px_block": self.pm_plan % 100000000 // 1000} \
                 if self.pm_plan else "one lane per pixel"
         return cfg
 
@@ -837,18 +839,29 @@ class RbfPerPixelWorkload(Workload):
         self.L, self.lib = L, L.lib()
         self.stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
-    def step(self, i):
+    def step(self, i, fallback=None):
         c, L = ctypes, self.L
-        st = self.lib.rti_rbf_perpixel(c.c_void_p(self.lu.data_ptr()), c.c_void_p(self.lv.data_ptr()),
-                                       c.c_void_p(self.I.data_ptr()), L.RTI_I32, self.N, self.P,
-                                       c.c_void_p(self.luv.data_ptr()), self.E, c.c_void_p(self.out.data_ptr()),
-                                       L.RTI_I32, L.RTI_OUT_EVAL_MAJOR, c.c_void_p(self.status.data_ptr()),
-                                       self.stream)
+        st = self.lib.rti_rbf_perpixel_ex(c.c_void_p(self.lu.data_ptr()), c.c_void_p(self.lv.data_ptr()),
+                                          c.c_void_p(self.I.data_ptr()), L.RTI_I32, self.N, self.P,
+                                          c.c_void_p(self.luv.data_ptr()), self.E, c.c_void_p(self.out.data_ptr()),
+                                          L.RTI_I32, L.RTI_OUT_EVAL_MAJOR, c.c_void_p(self.status.data_ptr()),
+                                          c.c_void_p(fallback.data_ptr() if fallback is not None else None),
+                                          self.stream)
         if st:
-            L.check(st, "rti_rbf_perpixel")
+            L.check(st, "rti_rbf_perpixel_ex")
+
+    def fallback_px(self):
+        """Pixels one step hands to the fp64 partial-pivoting fallback (81 <= N <= 256; 0 otherwise)."""
+        import torch
+
+        cnt = torch.zeros(1, dtype=torch.int32, device=self.I.device)
+        self.step(0, cnt)
+        torch.cuda.synchronize(self.I.device)
+        return int(cnt.item())
 
     def config(self):
-        return {"lights": self.N, "evals": self.E, "basis": "rbf-linear per-pixel", "out": "int32 tables [E][P]"}
+        return {"lights": self.N, "evals": self.E, "basis": "rbf-linear per-pixel", "out": "int32 tables [E][P]",
+                "fallback_px": self.fallback_px()}
 
     def roofline(self, kernel_ms):
         ach = self.flops / (kernel_ms * 1e-3) / 1e12
@@ -994,7 +1007,9 @@ def allgather_legs(wl, ctx, reps=5):
     torch.cuda.synchronize(dev)
     gather_ms = (time.perf_counter() - t0) / reps * 1e3
     # cyclic blocks of H/(G*chunks) rows (4K on 8 GPUs: 2160/8 = 270 rows per rank -> 3 chunks of 90)
-    chunks = next(c for c in (4, 3, 2, 1) if ctx.H % (ctx.world * c) == 0)
+    if ctx.H % ctx.world:  # the block-cyclic leg needs equal row blocks on every rank
+        return gather_ms, None, 0, {"skipped": f"H={ctx.H} is not a multiple of {ctx.world} ranks", "ok": True}
+    chunks = next((c for c in (4, 3, 2, 1) if ctx.H % (ctx.world * c) == 0), 1)
     I_cyc = cyclic_stack(wl, ctx, chunks)
     fitter = RowTiledFitter(I_cyc, wl.lu, wl.lv, ctx.H, basis=wl.basis, chunks=chunks, partition="cyclic")
     for _ in range(2):
@@ -1084,6 +1099,8 @@ def main():
     kind = cfg[0]
     if args.stack == "pixel" and kind != "fit":
         raise SystemExit("--stack pixel applies to the fit configs (c2, c3, c4)")
+    if args.kernel in ("q8", "h16") and (kind not in ("fit",) or args.in_dtype != "u8"):
+        raise SystemExit(f"--kernel {args.kernel} is the 8-bit fit: it needs a fit config and --in-dtype u8")
     if args.steps is None:
         args.steps = DEFAULT_STEPS[kind]
 
@@ -1186,7 +1203,8 @@ def main():
     gather_ms = e2e_ms = e2e_par = None
     if world > 1 and kind == "fit" and not args.no_allgather:
         gather_ms, e2e_ms, n_chunks, e2e_par = allgather_legs(wl, ctx)
-        gather_ms, e2e_ms = reduce_max([gather_ms, e2e_ms], ctx, backend)
+        gather_ms, e2e_ms = reduce_max([gather_ms, e2e_ms if e2e_ms is not None else 0.0], ctx, backend)
+        e2e_ms = e2e_ms or None
 
     value = wl.total_units * args.steps / elapsed / 1e6
     cpu = None
@@ -1224,9 +1242,10 @@ def main():
         }
         if gather_ms is not None:
             line["allgather_ms"] = round(gather_ms, 3)
-            line["fit_allgather_overlapped_ms"] = round(e2e_ms, 3)  # row chunks, gather(c) || fit(c+1)
-            line["overlap_chunks"] = int(n_chunks)
-            line["end_to_end_Mpix_lights_per_s"] = round(wl.total_units / (e2e_ms * 1e-3) / 1e6, 1)
+            if e2e_ms is not None:
+                line["fit_allgather_overlapped_ms"] = round(e2e_ms, 3)  # row chunks, gather(c) || fit(c+1)
+                line["overlap_chunks"] = int(n_chunks)
+                line["end_to_end_Mpix_lights_per_s"] = round(wl.total_units / (e2e_ms * 1e-3) / 1e6, 1)
             line["e2e_parity"] = e2e_par
         print(json.dumps(line), flush=True)
     if world > 1:

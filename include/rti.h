@@ -146,19 +146,26 @@ int rti_fit_shared(const float* pinv, int k, int N,
  *   coef[c][p][i] = Σ_n pinv[i][n] · I[c*channel_stride + p*pixel_stride + n]
  * (pixel_stride 0 = N, channel_stride 0 = P*pixel_stride).  pinv, coef, coef_layout and
  * coef_channel_stride as rti_fit_shared; in_dtype F32 / I32 / U8.
- * AUTO (and RTI_KERNEL_MFMA) streams whole blocks of 16·G consecutive pixels (one contiguous run of
- * 16·G·N values) HBM -> LDS by LDS-DMA and contracts them with v_mfma_f32_16x16x4_f32: F32 / I32 stacks,
- * k in {6, 9, 16}, pixel_stride = N, P·N and channel_stride multiples of 4, I and coef 16-byte aligned,
- * P·k·4 < 2^31 and N within the LDS budget (rti_fit_shared_pm_plan).  RTI_KERNEL_MFMA fails with
- * RTI_ERR_UNSUPPORTED outside that; AUTO and RTI_KERNEL_VALU run one lane per pixel instead (any shape).
- * kernel: RTI_KERNEL_CHUNKS(G) (G in {1, 2, 4}) and RTI_KERNEL_TILE_WAVES(W) override the block and the
- * waves per workgroup (measurement). */
+ * AUTO streams runs of 16-pixel groups (contiguous 16·N values each) HBM -> a per-wave LDS ring by 1-KiB
+ * LDS-DMAs and contracts them there: one pixel per lane with packed FMAs for k <= 9, v_mfma_f32_16x16x4_f32
+ * for k = 16 (RTI_KERNEL_MFMA: the MFMA stream for every k; RTI_KERNEL_TILE: a double-buffered block form).
+ * These take F32 / I32 stacks, k in {6, 9, 16}, pixel_stride = N, P·N and channel_stride multiples of 4,
+ * I and coef 16-byte aligned, P·k·4 < 2^31 and N within the LDS budget (rti_fit_shared_pm_plan);
+ * RTI_KERNEL_MFMA / TILE fail with RTI_ERR_UNSUPPORTED outside that, AUTO and RTI_KERNEL_VALU run one lane
+ * per pixel instead (any shape, uint8 included).  Measurement flags: RTI_KERNEL_TILE_WAVES(W) waves per
+ * workgroup, RTI_KERNEL_CHUNKS(n) (MFMA stream: n× the smallest unit; block form: 16n-pixel blocks),
+ * RTI_KERNEL_ROTATE (MFMA stream: each wave one contiguous run of units). */
 int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
                       int64_t pixel_stride, int64_t channel_stride,
                       float* coef, int coef_layout, int64_t coef_channel_stride,
                       int kernel, rti_stream_t stream);
-/* 0 if rti_fit_shared_pm's DMA/MFMA kernel does not take this shape, else its plan:
- * 1000·(pixels per block) + waves per workgroup. */
+/* 0 if rti_fit_shared_pm runs one lane per pixel (the fallback) for this shape and kernel selection, else
+ * form·10^8 + size·1000 + W: form RTI_PM_VALU_STREAM (AUTO, k <= 9: one pixel per lane, packed FMAs) or
+ * RTI_PM_MFMA_STREAM (AUTO k = 16, RTI_KERNEL_MFMA) with size = KiB of LDS ring per wave, or RTI_PM_BLOCK
+ * (RTI_KERNEL_TILE, or N too small for a ring) with size = pixels per block; W = waves per workgroup. */
+#define RTI_PM_VALU_STREAM 1
+#define RTI_PM_MFMA_STREAM 2
+#define RTI_PM_BLOCK       3
 int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int C, int64_t pixel_stride,
                            int64_t channel_stride, int kernel);
 
@@ -188,7 +195,10 @@ int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I, int64_t P,
  * the fp32 stream, a quarter of the q8 form's accumulator registers per pixel, so 2048-pixel tiles and
  * 2-KiB runs per wave and plane.  rti_h16_operator builds the operator (rti_h16_operator_bytes(k, N)
  * bytes, device copy 16-byte aligned) from the fp64 pseudo-inverse (non-finite entries -> RTI_ERR_BAD_ARG).
- * Arguments, alignment and layouts as rti_fit_shared_q8; N <= rti_fit_shared_h16_max_lights(). */
+ * Arguments, alignment and layouts as rti_fit_shared_q8; N <= rti_fit_shared_h16_max_lights().
+ * op (here and for rti_fit_shared_q8) must be the operator built for the SAME k and N: the kernel copies
+ * rti_*_operator_bytes(k, N) bytes of it into LDS and the buffer carries no size the ABI could check
+ * (the Python layer checks the tensor's size). */
 int64_t rti_h16_operator_bytes(int k, int N);
 int rti_h16_operator(const double* pinv, int k, int N, void* op);
 int rti_fit_shared_h16_max_lights(void);
@@ -321,10 +331,20 @@ int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp,
  * [y][x][ly][lx]) or RTI_OUT_EVAL_MAJOR ([e][p], prepare_images_data's [ly][lx][y][x]).
  * status: device int the caller zeroes; set to RTI_ERR_SINGULAR when a pixel's system is
  * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 2556
- * (RTI_ERR_UNSUPPORTED above: the Cholesky panel's LDS). */
+ * (RTI_ERR_UNSUPPORTED above: the Cholesky panel's LDS).
+ * Device memory: the call allocates (stream-ordered, hipMallocAsync) and frees a workspace of
+ * P·N·(8 + 8) bytes (weights + nodes) plus, for N > 256, one Cholesky slot of ≈ 8·(N+pad)² bytes per
+ * workgroup on min(P, CUs) workgroups (≈ 13.4 GB at N = 2556, 6.6 GB at N = 1800 on 256 CUs), or for
+ * 81 <= N <= 256 an fp64 fallback slot of 8·N·(N+1) bytes per CU; RTI_ERR_HIP if it cannot. */
 int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                      const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
                      rti_stream_t stream);
+/* The same, and fallback_px (NULL, or a device int the caller zeroes) receives the number of pixels the
+ * fp32-inverse solvers (81 <= N <= 256) handed to the fp64 partial-pivoting fallback (ill-conditioned:
+ * nearly repeated light directions). */
+int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
+                        const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
+                        int* fallback_px, rti_stream_t stream);
 
 /* ---- device: light vectors ---------------------------------------------------------
  * The light-vector half of compute_intensities (analysis.py:221-231) for an

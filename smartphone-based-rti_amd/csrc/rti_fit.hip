@@ -513,7 +513,8 @@ fit_shared_tile(const float* __restrict__ pinv, int k, int N, const T* __restric
 // as the waves grow and the registers go to loads in flight instead.
 // AHEAD = 0: ONE LDS tile (half the LDS, so twice the tile width fits: 16 KiB runs per wave and
 // plane at RC = 16), the next step's loads in registers during the compute, two barriers per step.
-template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT, bool STORE = true>
+// STORE: 1 plain coefficient stores, 2 non-temporal (RTI_KERNEL_NT_STORE, measurement), 0 none (probe)
+template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT, int STORE = 1>
 __global__ void __launch_bounds__(64 * W)
 fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P, int64_t pb,
                   int64_t pe, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
@@ -611,7 +612,7 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
   }
   // acc[g][c][rr] = coefficient 4r + rr of pixel t0 + pw + 64g + 4q + c
   float* __restrict__ dst = coef + (int64_t)blockIdx.y * ocstride;
-  if constexpr (!STORE) {  // measurement probe (tools/probe/tile_probe.hip): the read stream alone
+  if constexpr (STORE == 0) {  // measurement probe (tools/probe/tile_probe.hip): the read stream alone
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -620,6 +621,12 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
     if (t == -1.2345f) dst[0] = t;  // keeps the loads and MFMAs alive
     return;
   }
+  auto st16 = [&](float* p, floatx4 v) {
+    if constexpr (STORE == 2)
+      __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
+    else
+      *reinterpret_cast<floatx4*>(p) = v;
+  };
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int64_t px = t0 + pw + 64 * g + 4 * q;
@@ -628,13 +635,11 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int i = 4 * r + rr;
-        if (i < k)
-          *reinterpret_cast<floatx4*>(dst + (int64_t)i * P + px) =
-              floatx4{acc[g][0][rr], acc[g][1][rr], acc[g][2][rr], acc[g][3][rr]};
+        if (i < k) st16(dst + (int64_t)i * P + px, floatx4{acc[g][0][rr], acc[g][1][rr], acc[g][2][rr], acc[g][3][rr]});
       }
     } else if (k == 16) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) *reinterpret_cast<floatx4*>(dst + (px + c) * 16 + 4 * r) = acc[g][c];
+      for (int c = 0; c < 4; ++c) st16(dst + (px + c) * 16 + 4 * r, acc[g][c]);
     } else {
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -1072,14 +1077,14 @@ int launch_tile_l(const FitArgs& a) {
               : launch_tile_t<RC, SP, T, RTI_COEF_PIXEL_MAJOR, false>(a);
 }
 
-template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT>
+template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT, int STORE = 1>
 int launch_tile_w_t(const FitArgs& a) {
   constexpr int R = 256 * RC, S = W;
   const int T_ = (a.N + S - 1) / S;
   const size_t lds = ((size_t)T_ * S * 16 + (size_t)(AHEAD == 0 ? 1 : 2) * S * R) * sizeof(float);
   if (lds > 160 * 1024)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
-  auto kern = fit_shared_tile_w<RC, W, AHEAD, T, LAYOUT, NT>;
+  auto kern = fit_shared_tile_w<RC, W, AHEAD, T, LAYOUT, NT, STORE>;
   if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
@@ -1093,6 +1098,11 @@ int launch_tile_w_t(const FitArgs& a) {
 // wide-workgroup tile (fp32): rc 4 or 8, 8 waves, loads 1 or 2 steps ahead
 template <int RC, int AHEAD, int W = 8>
 int launch_tile_w_l(const FitArgs& a) {
+  if constexpr (RC == 16 && AHEAD == 0) {  // AUTO's kernel with non-temporal coefficient stores (measurement)
+    if ((a.mode & VM_NTS) && a.nt)
+      return a.layout == RTI_COEF_PLANAR ? launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, true, 2>(a)
+                                         : launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PIXEL_MAJOR, true, 2>(a);
+  }
   if (a.layout == RTI_COEF_PLANAR)
     return a.nt ? launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, true>(a)
                 : launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, false>(a);
@@ -1123,7 +1133,7 @@ int launch_tile_s_t(const FitArgs& a) {
   const dim3 grid((unsigned)(ntot < cus ? ntot : cus));
   hipLaunchKernelGGL(kern, grid, dim3(64 * W), lds, a.stream, a.pinv, a.k, a.N, static_cast<const float*>(a.I), a.P,
                      tpc, ntot, a.lstride, a.cstride, a.coef, a.ocstride);
-  return RTI_OK;
+  return check_launch("rti_fit_shared");
 }
 
 int launch_tile_s(const FitArgs& a) {
@@ -1364,7 +1374,8 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     // PTM-6 pixel-major coefficients leave through LDS as whole 1 KiB rows per store
     // instruction: with wide lanes the direct 96-B-strided stores raised WRITE_SIZE to 1.46x
     // the coefficient bytes (c3 0.573 -> 0.549 ms, c2 0.082 -> 0.072 ms staged)
-    a.mode = VM_NT | (k == 6 ? VM_STAGE : 0) | ((kernel & RTI_KERNEL_ROTATE) ? VM_ROT : 0);
+    a.mode = VM_NT | (k == 6 ? VM_STAGE : 0) | ((kernel & RTI_KERNEL_ROTATE) ? VM_ROT : 0) |
+             ((k == 16 && (kernel & RTI_KERNEL_NT_STORE)) ? VM_NTS : 0);
   }
   Generations gens;  // one launch unless AUTO splits it (launch generations, above)
   if (a.nc == 0) {
@@ -1420,7 +1431,8 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
       // (16 KiB per wave and plane; c4 3.74 vs 3.93 ms for the 2048-pixel double-buffered tile,
       // profiles/r02_c4_tile_rc16_sweep.log); above N = 512 its [N][16] pinv no longer fits.
       const bool tile_auto =
-      (kernel & ~0xff & ~(RTI_KERNEL_NONTEMPORAL | RTI_KERNEL_ONE_LAUNCH | RTI_KERNEL_ROUNDS)) == 0 && N <= 512;
+      (kernel & ~0xff & ~(RTI_KERNEL_NONTEMPORAL | RTI_KERNEL_ONE_LAUNCH | RTI_KERNEL_ROUNDS | RTI_KERNEL_NT_STORE)) == 0 &&
+      N <= 512;
       const int rc0 = rc ? rc : (N <= 512 ? 8 : 4);
       int st;
       switch (in_dtype) {

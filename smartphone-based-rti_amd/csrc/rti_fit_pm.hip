@@ -403,13 +403,15 @@ fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
 // units and channels: each lane keeps its own group cursor, and the coefficients leave by buffer stores
 // over the WHOLE coefficient array (per-lane 32-bit offsets; lanes past P or past the stream get an
 // out-of-range offset), so every block issues the same SB stores.
-template <int K, typename T, int LAYOUT, int ALIGN>
+// MODE (measurement, rti_fit_shared_pm flags): 0 = the fit; 1 = no coefficient stores (RTI_KERNEL_ONE_LAUNCH);
+// 2 = no arithmetic, the stream waited for and zeros stored (RTI_KERNEL_ROUNDS)
+template <int K, typename T, int LAYOUT, int ALIGN, int MODE = 0>
 __global__ void __launch_bounds__(256)
 fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
                float* __restrict__ coef, int64_t ocstride, int C, int U, int nu, int64_t tu, int ring,
                uint32_t coef_bytes) {
   typedef float f2 __attribute__((ext_vector_type(2)));
-  constexpr int SB = LAYOUT == RTI_COEF_PIXEL_MAJOR ? (K % 2 == 0 ? K / 2 : K) : K;  // stores per block
+  constexpr int SB = MODE == 1 ? 0 : (LAYOUT == RTI_COEF_PIXEL_MAJOR ? (K % 2 == 0 ? K / 2 : K) : K);  // stores per block
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int W = blockDim.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -493,8 +495,8 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
     float acc1[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) acc1[i] = 0.f;
-    int n = 0;
-    if constexpr (ALIGN == 4) {
+    int n = MODE == 2 ? N : 0;
+    if constexpr (ALIGN == 4 && MODE != 2) {
       // one step of 4 lights ahead: step n + 4's row values and weights are read (LDS: in order, counted
       // waits) while step n's 2·K packed FMAs issue
       auto rdx = [&](int nn) {
@@ -539,6 +541,13 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
     float c[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) c[i] = (acc[i][0] + acc[i][1]) + acc1[i];
+    if constexpr (MODE == 1) {  // measurement: keep the arithmetic, drop the stores
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < K; ++i) t += c[i];
+      if (t == -1.2345f) coef[0] = t;  // never taken for the bench's data (a plain store, not counted by SB)
+    } else
+    {
     // stores: pixel px of channel lc; lanes past the stream or past P drop theirs
     const int px = (lu * U + gi) * 16 + q;
     const bool ok = 4 * b + (lane >> 4) < ng && px < P;
@@ -556,6 +565,7 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
         const uint32_t off = ok ? cb + (uint32_t)(e * 4) : PM_OOB_ALL;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(c[i]), rs, off, 0, 0);
       }
+    }
     }
     // refill every KiB the blocks 0..b freed
     const int lim0 = (end + ring) >> 10;
@@ -609,6 +619,7 @@ struct PmArgs {
   int layout;
   int64_t ocs;
   hipStream_t stream;
+  int mode = 0;  // measurement variants of the VALU stream (fit_pm_vstream MODE)
 };
 
 // LDS plan of the DMA kernel: G groups of 16 pixels per block, W waves per workgroup
@@ -788,7 +799,8 @@ VPlan vstream_plan(int k, int N, size_t es, int w_req) {
 
 template <int K, typename T, int LAYOUT, int ALIGN>
 int launch_vstream_t(const PmArgs& a, const VPlan& pl) {
-  auto kern = fit_pm_vstream<K, T, LAYOUT, ALIGN>;
+  auto kern = a.mode == 1 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 1>
+                          : (a.mode == 2 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 2> : fit_pm_vstream<K, T, LAYOUT, ALIGN, 0>);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)pl.lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
@@ -865,16 +877,14 @@ extern "C" int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int
   const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
   if ((kernel & 0xff) == RTI_KERNEL_AUTO) {
     const VPlan vp = vstream_plan(k, N, 4, w_req);
-    if (vp.W && (int64_t)C * P * k * 4 < 0xFFFFFFF0ll)
-      return -(int)(((vp.ring >> 10) * 1000 + vp.W) + 100000000);  // VALU stream: −(1e8 + ring KiB·1000 + W)
+    if (vp.W && (int64_t)C * P * k * 4 < 0xFFFFFFF0ll) return RTI_PM_VALU_STREAM * 100000000 + (vp.ring >> 10) * 1000 + vp.W;
   }
   if ((kernel & 0xff) != RTI_KERNEL_TILE) {
     const StreamPlan sp = stream_plan(N, 4, w_req, c_req);
-    if (sp.W) return (sp.ring >> 10) * 1000 + sp.W;  // KiB of ring per wave · 1000 + waves per workgroup
+    if (sp.W) return RTI_PM_MFMA_STREAM * 100000000 + (sp.ring >> 10) * 1000 + sp.W;
   }
-  // the double-buffered block form (kernel TILE, or N < 16)
   const PmPlan pl = pm_plan(N, 4, (kernel & 0xff) == RTI_KERNEL_TILE ? c_req : 0, w_req);
-  return pl.G ? -(16 * pl.G * 1000 + pl.W) : 0;  // −(pixels per block · 1000 + waves per workgroup)
+  return pl.G ? RTI_PM_BLOCK * 100000000 + 16 * pl.G * 1000 + pl.W : 0;
 }
 
 extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
@@ -901,6 +911,7 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
   a.layout = coef_layout;
   a.ocs = coef_channel_stride ? coef_channel_stride : P * k;
   a.stream = (hipStream_t)stream;
+  a.mode = (kernel & RTI_KERNEL_ONE_LAUNCH) ? 1 : ((kernel & RTI_KERNEL_ROUNDS) ? 2 : 0);
   if (a.ps < N) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: pixel_stride < N");
   if (C > 1 && a.cs < P * a.ps) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: channel_stride");
   if (C > 1 && a.ocs < P * k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: coef_channel_stride");

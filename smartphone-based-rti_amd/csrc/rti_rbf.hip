@@ -818,7 +818,7 @@ template <typename T>
 __global__ void __launch_bounds__(RBF_FB_THREADS)
 rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
                const int* __restrict__ redo, double* __restrict__ ws, double* __restrict__ wT,
-               int* __restrict__ status) {
+               int* __restrict__ status, int* __restrict__ fallback_px) {
   __shared__ double xs[RBF_MAX_N], ys[RBF_MAX_N], lf[RBF_MAX_N];
   __shared__ int used[RBF_MAX_N];
   __shared__ double s_val[RBF_FB_THREADS / 64];
@@ -835,6 +835,7 @@ rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const
   if (first + t < P && redo[first + t]) s_list[atomicAdd(&s_count, 1)] = first + t;
   __syncthreads();
   const int count = s_count;
+  if (t == 0 && count > 0 && fallback_px) atomicAdd(fallback_px, count);  // (reported by rti_rbf_perpixel_ex)
   for (int li = 0; li < count; ++li) {
     const int64_t p = s_list[li];
     const int64_t base = p * N;
@@ -1281,7 +1282,8 @@ bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); 
 // redo / fb_ws: the flag per pixel (zeroed) and the fp64 fallback's workspace, when uses_gji(N)
 template <typename T>
 void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
-                  int* status, int* redo, double* fb_ws, int64_t chol_grid, int64_t fb_grid, hipStream_t s) {
+                  int* status, int* redo, double* fb_ws, int64_t chol_grid, int64_t fb_grid, int* fallback_px,
+                  hipStream_t s) {
   const T* In = static_cast<const T*>(I);
   const dim3 g((unsigned)P);
   if (N > RBF_MAX_N) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
@@ -1312,7 +1314,7 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
                          gji_refine());
     const unsigned fg = (unsigned)(P < fb_grid ? P : fb_grid);
     hipLaunchKernelGGL((rbf_solve_fp64<T>), dim3(fg), dim3(RBF_FB_THREADS), 0, s, lu, lv, In, N, P, redo, fb_ws, wT,
-                       status);
+                       status, fallback_px);
     return;
   }
 #define RBF_GJ(NM)                                                                                       \
@@ -1354,6 +1356,12 @@ using namespace rti;
 extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                                 const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
                                 rti_stream_t stream) {
+  return rti_rbf_perpixel_ex(lu, lv, I, in_dtype, N, P, luv, E, out, out_dtype, out_layout, status, nullptr, stream);
+}
+
+extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
+                                   const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
+                                   int* fallback_px, rti_stream_t stream) {
   if (!lu || !lv || !I || !luv || !out || !status) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: null pointer");
   if (N <= 0 || P <= 0 || E <= 0) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: N, P, E must be positive");
   if (N > RBF_CH_MAX_N)
@@ -1390,9 +1398,9 @@ extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I,
     return fail(RTI_ERR_HIP, "rti_rbf_perpixel: clearing the redo flags failed");
   }
   switch (in_dtype) {
-    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, s); break;
-    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, s); break;
-    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, s); break;
+    case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, fallback_px, s); break;
+    case RTI_I32: launch_solve<int32_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, fallback_px, s); break;
+    default: launch_solve<uint8_t>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, fallback_px, s); break;
   }
   switch (out_dtype) {
     case RTI_F64: launch_eval<double>(out_layout, wT, xyT, N, P, luv, E, out, s); break;

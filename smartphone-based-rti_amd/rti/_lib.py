@@ -44,6 +44,9 @@ RTI_KERNEL_PINV_LDS = 0x200
 RTI_KERNEL_NT_STORE = 0x400
 RTI_KERNEL_STAGE = 0x800
 RTI_KERNEL_ROTATE = 0x10000000  # measurement variant: per-wave rotated light order (AUTO PTM-6 fp32)
+RTI_PM_VALU_STREAM = 1  # rti_fit_shared_pm_plan forms (include/rti.h)
+RTI_PM_MFMA_STREAM = 2
+RTI_PM_BLOCK = 3
 RTI_KERNEL_ONE_LAUNCH = 0x20000000  # measurement variant: AUTO without launch generations
 RTI_KERNEL_ROUNDS = 0x40000000  # measurement variant: AUTO generations as rounds of one launch
 RTI_KERNEL_CHUNKS_SHIFT = 12  # VALU chunks per lane in bits 12-15 (0 = AUTO)
@@ -124,6 +127,8 @@ SIGNATURES = {
                                         _c_i64, _c_int, _c_i64, _c_i64, _c_void_p, _c_int, _c_i64, _c_i64, _c_void_p]),
     "rti_rbf_perpixel": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_i64, _c_void_p, _c_int,
                                   _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p]),
+    "rti_rbf_perpixel_ex": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_i64, _c_void_p, _c_int,
+                                     _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p, _c_void_p]),
     "rti_relight": (_c_int, [_c_void_p, _c_int, _c_int, _c_i64, _c_int, _c_void_p, _c_int, _c_void_p, _c_int,
                              _c_int, _c_void_p]),
     "rti_relight_frame": (_c_int, [_c_void_p, _c_int, _c_int, _c_int, _c_i64, _c_double, _c_double, _c_void_p,

@@ -142,6 +142,15 @@ def h16_operator(pinv64):
     return op
 
 
+def _check_operator(op_dev, nbytes, form, k, N):
+    """The kernels copy exactly rti_*_operator_bytes(k, N) bytes of the operator into LDS: one built for
+    another (k, N) would be read out of range or misread, so its size must match (the C ABI cannot check
+    a device buffer it is not given the size of)."""
+    if op_dev.dtype != torch.uint8 or op_dev.numel() != nbytes:
+        raise ValueError(f"{form} operator of {op_dev.numel()} {op_dev.dtype} elements, expected {nbytes} uint8 "
+                         f"bytes for k={k}, N={N}: build it with rti.{form}_operator(pinv) for this light set")
+
+
 def fit_h16_into(op_dev, I, coef, *, k, layout="pixel", flags=0):
     """Launch ``rti_fit_shared_h16`` on preallocated tensors: op_dev = h16_operator(...) on the device
     (uint8), I a contiguous uint8 CUDA [N, P] or [C, N, P] stack, coef fp32 as fit_shared_into."""
@@ -149,6 +158,7 @@ def fit_h16_into(op_dev, I, coef, *, k, layout="pixel", flags=0):
         C, (N, P) = 1, I.shape
     else:
         C, N, P = I.shape
+    _check_operator(op_dev, int(L.lib().rti_h16_operator_bytes(k, N)), "h16", k, N)
     st = L.lib().rti_fit_shared_h16(_vp(op_dev), k, N, _vp(I), P, C, P, N * P, _vp(coef), _layout_id(layout),
                                     P * k, int(flags), _stream_of(I))
     L.check(st, "rti_fit_shared_h16")
@@ -171,6 +181,7 @@ def fit_q8_into(op_dev, I, coef, *, k, layout="pixel", flags=0):
         C, (N, P) = 1, I.shape
     else:
         C, N, P = I.shape
+    _check_operator(op_dev, int(L.lib().rti_q8_operator_bytes(k, N)), "q8", k, N)
     st = L.lib().rti_fit_shared_q8(_vp(op_dev), k, N, _vp(I), P, C, P, N * P, _vp(coef), _layout_id(layout), P * k,
                                    int(flags), _stream_of(I))
     L.check(st, "rti_fit_shared_q8")

@@ -19,7 +19,8 @@ def test_golden_256x256_N20_pixel_major(cuda):
     compute_intensities builds it, and as a permuted view of that layout."""
     d = golden("ptm_shared_256x256_N20.npz")
     Ipm = torch.as_tensor(np.ascontiguousarray(np.moveaxis(d["I"], 0, -1))).to(cuda, torch.float32)  # [256, 256, 20]
-    assert L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, 0) > 0  # the DMA/MFMA kernel
+    plan = L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, 0)
+    assert plan // 10**8 == L.RTI_PM_VALU_STREAM, plan  # AUTO for PTM-6: the packed-FMA stream
     for layout in ("pixel", "planar"):
         coef = rti.fit(Ipm, d["lu"], d["lv"], stack="pixel", layout=layout).cpu().numpy()
         if layout == "planar":

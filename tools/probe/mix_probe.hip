@@ -173,6 +173,11 @@ extern "C" int probe_mix_px(const float* I, int N, int64_t P, float* out, int nc
   if (nc == 4 && outf == 6) return launch_px<4, 6>(I, N, P, out, place, launches, s);
   if (nc == 8 && outf == 6) return launch_px<8, 6>(I, N, P, out, place, launches, s);
   if (nc == 2 && outf == 6) return launch_px<2, 6>(I, N, P, out, place, launches, s);
+  // 8-bit stacks viewed as 4-byte words (16 pixels per lane chunk, 24 output floats per word = PTM-6 fp32)
+  if (nc == 1 && outf == 24) return launch_px<1, 24>(I, N, P, out, place, launches, s);
+  if (nc == 2 && outf == 24) return launch_px<2, 24>(I, N, P, out, place, launches, s);
+  if (nc == 4 && outf == 24) return launch_px<4, 24>(I, N, P, out, place, launches, s);
+  if (nc == 8 && outf == 24) return launch_px<8, 24>(I, N, P, out, place, launches, s);
   return 2;
 }
 
@@ -195,7 +200,7 @@ __device__ __forceinline__ void glds16(const float* g, float* l) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 2);
 }
 
-template <int D, bool DMA, int ORDER>
+template <int D, bool DMA, int ORDER, int BURST = 1>
 __global__ void __launch_bounds__(512) pm_read(const float* __restrict__ I, int64_t kib, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float ring[];
   const int lane = threadIdx.x & 63;
@@ -212,11 +217,21 @@ __global__ void __launch_bounds__(512) pm_read(const float* __restrict__ I, int6
 #pragma unroll
     for (int i = 0; i < D; ++i)
       glds16(kaddr(i), rb + i * 256);
-    for (int64_t i = D; i < per; ++i) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 1) : "memory");
-      const int s = (int)(i % D);
-      acc += *reinterpret_cast<const floatx4*>(rb + s * 256 + 4 * lane);
-      glds16(kaddr(i), rb + s * 256);
+    if constexpr (BURST == 1) {
+      for (int64_t i = D; i < per; ++i) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 1) : "memory");
+        const int s = (int)(i % D);
+        acc += *reinterpret_cast<const floatx4*>(rb + s * 256 + 4 * lane);
+        glds16(kaddr(i), rb + s * 256);
+      }
+    } else if constexpr (D > BURST) {  // the fits' shape: wait for BURST KiB, consume them, refill BURST KiB
+      for (int64_t i = D; i + BURST <= per; i += BURST) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - BURST) : "memory");
+#pragma unroll
+        for (int b = 0; b < BURST; ++b) acc += *reinterpret_cast<const floatx4*>(rb + ((i + b) % D) * 256 + 4 * lane);
+#pragma unroll
+        for (int b = 0; b < BURST; ++b) glds16(kaddr(i + b), rb + ((i + b) % D) * 256);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
@@ -238,6 +253,13 @@ int launch_pm_read(const float* I, int64_t bytes, float* out, int dma, int order
   const int cus = 256;
   const size_t lds = dma ? (size_t)waves * D * 1024 : 0;
   const dim3 grid(cus), block(64 * waves);
+#define PMRB(OR)                                                                                             \
+  {                                                                                                          \
+    if (lds > 65536)                                                                                         \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pm_read<D, true, OR, 6>),                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                       \
+    hipLaunchKernelGGL((pm_read<D, true, OR, 6>), grid, block, lds, s, I, kib, out);                          \
+  }
 #define PMR(DM, OR)                                                                                          \
   {                                                                                                          \
     if (lds > 65536)                                                                                         \
@@ -245,8 +267,11 @@ int launch_pm_read(const float* I, int64_t bytes, float* out, int dma, int order
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                       \
     hipLaunchKernelGGL((pm_read<D, DM, OR>), grid, block, lds, s, I, kib, out);                               \
   }
-  if (dma && order) PMR(true, 1) else if (dma) PMR(true, 0) else if (order) PMR(false, 1) else PMR(false, 0)
+  if (dma == 2) {  // bursts of 6 KiB (a 16-pixel group of 100 lights)
+    if (order) PMRB(1) else PMRB(0)
+  } else if (dma && order) PMR(true, 1) else if (dma) PMR(true, 0) else if (order) PMR(false, 1) else PMR(false, 0)
 #undef PMR
+#undef PMRB
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -259,7 +284,7 @@ extern "C" int probe_pm_read(const float* I, int64_t bytes, float* out, int dma,
   if (waves < 1 || waves > 8 || (bytes >> 10) % (256 * waves) || (bytes >> 10) / (256 * waves) < depth) return 2;
   if (dma && (size_t)waves * depth * 1024 > 160 * 1024) return 2;
   switch (depth) {
-    case 4: return launch_pm_read<4>(I, bytes, out, dma, order, waves, s);
+    case 4: return dma == 2 ? 2 : launch_pm_read<4>(I, bytes, out, dma, order, waves, s);
     case 8: return launch_pm_read<8>(I, bytes, out, dma, order, waves, s);
     case 16: return launch_pm_read<16>(I, bytes, out, dma, order, waves, s);
     default: return 2;

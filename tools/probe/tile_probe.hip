@@ -8,7 +8,7 @@ extern "C" int probe_tile_nostore(const float* pinv, int k, int N, const float* 
   constexpr int RC = 16, W = 8, R = 256 * RC, S = W;
   const int T_ = (N + S - 1) / S;
   const size_t lds = ((size_t)T_ * S * 16 + (size_t)S * R) * sizeof(float);
-  auto kern = rti::fit_shared_tile_w<RC, W, 0, float, RTI_COEF_PIXEL_MAJOR, true, false>;
+  auto kern = rti::fit_shared_tile_w<RC, W, 0, float, RTI_COEF_PIXEL_MAJOR, true, 0>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return 3;

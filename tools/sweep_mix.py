@@ -28,17 +28,18 @@ PLACES = {0: "reads only", 1: "stores after sweep", 2: "stores spread", 3: "stor
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c3", choices=["c3", "c4", "pm"],
+    ap.add_argument("--config", default="c3", choices=["c3", "c4", "pm", "u8"],
                     help="pm: 1-KiB-per-instruction streams over the c3 stack's bytes (LDS-DMA vs registers)")
     ap.add_argument("--rounds", type=int, default=20)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    _, H, W, N, C, basis, _ = bench.CONFIGS["c3" if args.config == "pm" else args.config]
+    _, H, W, N, C, basis, _ = bench.CONFIGS["c3" if args.config in ("pm", "u8") else args.config]
     k = rti.basis_terms(basis)
     P = H * W
     lu, lv = bench.synth_dirs(N, 2)
     I = bench.synth_stack(H, W, N, C, basis, lu, lv, 1000, dev)
     pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=dev)
+    h16op = torch.as_tensor(rti.api.h16_operator(rti.pinv(lu, lv, basis)), device=dev) if args.config == "u8" else None
     coef = torch.empty((C, P, k), device=dev)
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "probe", "libmix_probe.so"))
     lib.probe_mix_px.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
@@ -49,15 +50,26 @@ def main():
     sp = ctypes.c_void_p(stream.cuda_stream)
     ip, op = ctypes.c_void_p(I.data_ptr()), ctypes.c_void_p(coef.data_ptr())
     variants = [("fit_auto", lambda: rti.fit_shared_into(pv, I, coef, k=k, layout="pixel", kernel="auto"))]
-    if args.config == "pm":
+    if args.config == "u8":  # the c3 stack as uint8: P bytes per plane = P/4 words, 16 pixels per 16-B lane chunk
+        I8 = I.to(torch.uint8)
+        i8 = ctypes.c_void_p(I8.data_ptr())
+        variants = [("fit_h16_auto", lambda: rti.api.fit_h16_into(h16op, I8, coef, k=k, layout="pixel"))]
+        for nc, launches in ((1, 1), (2, 1), (4, 1), (8, 1), (2, 4), (4, 4), (8, 4)):
+            for place in (0, 1):
+                variants.append((f"mix_u8_nc{nc}_L{launches}_p{place}",
+                                 (lambda nc=nc, launches=launches, place=place:
+                                  lib.probe_mix_px(i8, N, P // 4, op, nc, 24, place, launches, sp))))
+    elif args.config == "pm":
         lib.probe_pm_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         nbytes = (I.numel() * 4) // (1024 * 256 * 8) * (1024 * 256 * 8)
-        for dma in (1, 0):
+        for dma in (2, 1, 0):  # 2: LDS-DMA in bursts of 6 KiB (wait 6, refill 6), the fits' shape
             for order in (1, 0):
                 for waves in (8, 4):
                     for depth in (8, 16):
-                        variants.append((f"pm_read_{'dma' if dma else 'reg'}_{'slab' if order else 'runs'}_w{waves}_d{depth}",
+                        if dma == 2 and depth < 8:
+                            continue
+                        variants.append((f"pm_read_{['reg', 'dma', 'dmaburst6'][dma]}_{'slab' if order else 'runs'}_w{waves}_d{depth}",
                                          (lambda dma=dma, order=order, waves=waves, depth=depth:
                                           lib.probe_pm_read(ip, nbytes, op, dma, order, waves, depth, sp))))
     elif args.config == "c3":
@@ -86,7 +98,7 @@ def main():
             b.record(stream)
             times[name].append((a, b))
         torch.cuda.synchronize()
-    rbytes, wbytes = 4.0 * P * N * C, 4.0 * P * k * C
+    rbytes, wbytes = (1.0 if args.config == "u8" else 4.0) * P * N * C, 4.0 * P * k * C
     res = {}
     for name, _ in variants:
         ms = float(np.median([a.elapsed_time(b) for a, b in times[name]]))

@@ -48,7 +48,7 @@ def main():
         fl = w << L.RTI_KERNEL_TILE_WAVES_SHIFT
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl | L.RTI_KERNEL_MFMA)
         if plan:
-            variants.append((f"pm_stream_w{w}_ring{plan // 1000}K",
+            variants.append((f"pm_stream_w{w}_ring{plan % 100000000 // 1000}K",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="mfma", flags=fl)))
         if plan and w == 8:
             for u in (2, 4):
@@ -62,21 +62,26 @@ def main():
         fl = g << L.RTI_KERNEL_CHUNKS_SHIFT
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl | L.RTI_KERNEL_TILE)
         if plan:
-            variants.append((f"pm_block_{abs(plan) // 1000}px_w{abs(plan) % 1000}",
+            variants.append((f"pm_block_{plan % 100000000 // 1000}px_w{plan % 1000}",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="tile", flags=fl)))
     for w in (4, 3, 2):
         fl = w << L.RTI_KERNEL_TILE_WAVES_SHIFT
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
-        if plan <= -100000000:
-            variants.append((f"pm_valu_w{w}_ring{(-plan - 100000000) // 1000}K",
+        if plan // 100000000 == L.RTI_PM_VALU_STREAM:
+            variants.append((f"pm_valu_w{w}_ring{plan % 100000000 // 1000}K",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
     variants.append(("pm_auto", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto")))
+    if k <= 9:  # measurement variants of the VALU stream: no stores / no arithmetic
+        variants.append(("pm_valu_nostores", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
+                                                                              flags=L.RTI_KERNEL_ONE_LAUNCH)))
+        variants.append(("pm_valu_noarith", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
+                                                                             flags=L.RTI_KERNEL_ROUNDS)))
     agree = {}
     for name, fn in variants:
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        if name != "light_major_auto":
+        if name not in ("light_major_auto", "pm_valu_nostores", "pm_valu_noarith"):
             scale = ref.abs().amax(-1, keepdim=True).clamp_min(1e-30)
             agree[name] = float(((coef - ref).abs() / scale).max())
             coef.fill_(float("nan"))
