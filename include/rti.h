@@ -166,6 +166,7 @@ int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I, int in_dty
 #define RTI_PM_VALU_STREAM 1
 #define RTI_PM_MFMA_STREAM 2
 #define RTI_PM_BLOCK       3
+#define RTI_PM_DIRECT      4
 int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int C, int64_t pixel_stride,
                            int64_t channel_stride, int kernel);
 

@@ -51,6 +51,14 @@ __device__ __forceinline__ float to_f(T v) {
 }
 
 // 4 consecutive values of the LDS block at float offset `o` (aligned to ALIGN floats)
+// a 4-byte value of type T from its bits (passed as a scalar: a bit_cast of a vector element reads element 0,
+// clang / ROCm 7.2)
+template <typename T>
+__device__ __forceinline__ float bits_f(unsigned u) {
+  if constexpr (std::is_same<T, float>::value) return __uint_as_float(u);
+  else return (float)(int)u;
+}
+
 template <int ALIGN, typename T>
 __device__ __forceinline__ floatx4 lds4(const float* blk, int o) {
   const T* b = reinterpret_cast<const T*>(blk);
@@ -585,6 +593,103 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
   }
 }
 
+// DIRECT form (AUTO for N % 4 == 0, N <= 256): no LDS at all.  A wave streams 16-pixel groups (16·N
+// contiguous values) straight into VGPRs: for 16-light step s, lane (q, r) loads I[p0 + q][16s + 4r .. +3]
+// with one 16-byte buffer load, which is the B operand of four v_mfma_f32_16x16x4_f32 (MFMA j takes element
+// j: light 16s + 4r + j at k-index r, 16 pixels × 64 contiguous bytes per load instruction); the A operand,
+// pinv[q][16s + 4r + j], stays in VGPRs for the whole launch (4·NS values per lane).  D groups of loads are
+// in flight per wave.  Waves take groups gw, gw + GW, ... over the flattened (channel, group) space, so the
+// grid sweeps the stack as one contiguous window.  Lights past N and pixels past P are out-of-range buffer
+// offsets (they read zero and move no bytes), so no lane reads a neighbour pixel's values (a NaN stays in
+// its pixel).  The loads and MFMAs are plain straight-line code per group, so the compiler's own vmcnt
+// waits are exact: a group waits for its own loads only, with the next D − 1 groups' loads and the
+// previous groups' stores still in flight.
+// AUX: the loads' cache policy (2 = non-temporal: the stack is read once; 0 = plain, a measurement variant)
+template <int K, typename T, int LAYOUT, int NS, int D, int AUX = 2>
+__global__ void __launch_bounds__(256)
+fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
+              float* __restrict__ coef, int64_t ocstride, int ngrp, int g0, int tg, int contig) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, q = lane & 15, r = lane >> 4;
+  const int W = blockDim.x >> 6;
+  const int gw = (int)blockIdx.x * W + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), GW = (int)gridDim.x * W;
+  // this wave's groups of [g0, g0 + tg): gw, gw + GW, ... (interleaved) or one run of ⌈tg / GW⌉ (contig)
+  int first, step, ni;
+  if (contig) {
+    const int per = (tg + GW - 1) / GW;
+    first = gw * per;
+    step = 1;
+    ni = tg - first < per ? tg - first : per;
+  } else {
+    first = gw;
+    step = GW;
+    ni = gw < tg ? (tg - 1 - gw) / GW + 1 : 0;
+  }
+  if (ni <= 0) return;
+  first += g0;
+  float w[NS][4];
+  int off[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int n = 16 * s + 4 * r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[s][j] = (q < K && n + j < N) ? pinv[q * N + n + j] : 0.f;
+    off[s] = n < N ? (q * N + n) * (int)sizeof(T) : (int)PM_OOB;
+  }
+  const int gq = step / ngrp, gr = step - gq * ngrp;  // advance of a group cursor by one step
+  const int cbytes = (int)(P * K * 4);
+  // load cursor (the group D ahead) and store cursor (the group computed)
+  int lc = first / ngrp, lg = first - lc * ngrp, li = 0;
+  int sc = lc, sg = lg;
+  auto advance = [&](int& c, int& g) {
+    c += gq;
+    g += gr;
+    if (g >= ngrp) {
+      g -= ngrp;
+      ++c;
+    }
+  };
+  auto load = [&](u4 (&x)[NS]) {
+    const int64_t p0 = (int64_t)lg * 16;
+    const int rows = li < ni ? (int)(P - p0 < 16 ? P - p0 : 16) : 0;  // 0: past the stream, zero-traffic loads
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(I + (int64_t)lc * cstride + p0 * N), (short)0, rows * N * (int)sizeof(T), 0x00020000);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) x[s] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[s], 0, AUX);
+    ++li;
+    advance(lc, lg);
+  };
+  u4 x[D][NS];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    load(x[d]);
+    __builtin_amdgcn_sched_barrier(0);  // the prologue's groups in stream order
+  }
+  for (int i = 0; i < ni; i += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      // no exit inside the unrolled groups (the loop runs whole multiples of D; groups past the wave's last
+      // compute zeros and drop their stores): an exit there lets the compiler sink the loads behind it
+      __builtin_amdgcn_sched_barrier(0);
+      floatx4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[s][j], bits_f<T>(x[d][s][j]), acc[j], 0, 0,
+                                                        0);
+      load(x[d]);
+      const floatx4 c = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef + (int64_t)sc * ocstride, (short)0,
+                                                                          i + d < ni ? cbytes : 0, 0x00020000);
+      store_group<K, LAYOUT>(rs, c, (int64_t)sg * 16 + q, P, r);
+      advance(sc, sg);
+    }
+  }
+}
+
 // one lane per pixel: the fallback for every shape the DMA kernel does not take
 template <int K, typename T, int LAYOUT>
 __global__ void __launch_bounds__(256)
@@ -836,6 +941,65 @@ static bool vstream_coef_ok(const PmArgs& a) {
   return (uint64_t)a.ocs * (a.C - 1) * 4 + (uint64_t)a.P * a.k * 4 < 0xFFFFFFF0ull;
 }
 
+// DIRECT plan: NS 16-light steps (a bucket >= ceil(N / 16): the extra steps' loads are out of range, no bytes),
+// D groups of loads in flight per wave
+constexpr int pm_direct_ns(int N) {
+  return N <= 32 ? 2 : N <= 64 ? 4 : N <= 112 ? 7 : N <= 128 ? 8 : N <= 208 ? 13 : N <= 256 ? 16 : 0;
+}
+constexpr int pm_direct_depth(int ns) { return ns <= 4 ? 4 : ns <= 8 ? 3 : 2; }
+constexpr int PM_DIRECT_WPC = 8;  // waves per CU (AUTO)
+
+struct DirectOpts {
+  int wpc = PM_DIRECT_WPC;  // waves per CU
+  int gens = 1;             // launch generations (consecutive launches over equal group ranges)
+  int contig = 0;           // each wave one contiguous run of groups instead of interleaved groups
+  int nt = 1;               // non-temporal stack loads
+};
+
+template <int K, typename T, int LAYOUT, int NS>
+int launch_direct_t(const PmArgs& a, const DirectOpts& o) {
+  constexpr int D = pm_direct_depth(NS);
+  const int64_t ngrp = (a.P + 15) / 16, tg = ngrp * a.C;
+  if (tg >= ((int64_t)1 << 31) - 4096) return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: P too large");
+  const int64_t per = (tg + o.gens - 1) / o.gens;
+  int launches = 0;
+  for (int64_t g0 = 0; g0 < tg; g0 += per) {
+    const int64_t n = tg - g0 < per ? tg - g0 : per;
+    const int64_t wgs = (n + 3) / 4, cap = device_cus() * (int64_t)o.wpc / 4;
+    const unsigned grid = (unsigned)(wgs < cap ? wgs : (cap > 0 ? cap : 1));
+    auto kern = fit_pm_direct<K, T, LAYOUT, NS, D, 2>;
+    if constexpr (std::is_same<T, float>::value && LAYOUT == RTI_COEF_PIXEL_MAJOR && (NS == 7 || NS == 13))
+      if (!o.nt) kern = fit_pm_direct<K, T, LAYOUT, NS, D, 0>;  // measurement: plain loads (c3 / c4 shapes)
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, a.stream, a.pinv, a.N, static_cast<const T*>(a.I), a.P, a.cs,
+                       a.coef, a.ocs, (int)ngrp, (int)g0, (int)n, o.contig);
+    note_launches(++launches);
+  }
+  return RTI_OK;
+}
+
+template <int K, typename T, int LAYOUT>
+int launch_direct_n(const PmArgs& a, const DirectOpts& o) {
+  switch (pm_direct_ns(a.N)) {
+    case 2: return launch_direct_t<K, T, LAYOUT, 2>(a, o);
+    case 4: return launch_direct_t<K, T, LAYOUT, 4>(a, o);
+    case 7: return launch_direct_t<K, T, LAYOUT, 7>(a, o);
+    case 8: return launch_direct_t<K, T, LAYOUT, 8>(a, o);
+    case 13: return launch_direct_t<K, T, LAYOUT, 13>(a, o);
+    default: return launch_direct_t<K, T, LAYOUT, 16>(a, o);
+  }
+}
+
+template <typename T>
+int launch_direct(const PmArgs& a, const DirectOpts& o) {
+  const bool planar = a.layout == RTI_COEF_PLANAR;
+  switch (a.k) {
+    case 6: return planar ? launch_direct_n<6, T, RTI_COEF_PLANAR>(a, o) : launch_direct_n<6, T, RTI_COEF_PIXEL_MAJOR>(a, o);
+    case 9: return planar ? launch_direct_n<9, T, RTI_COEF_PLANAR>(a, o) : launch_direct_n<9, T, RTI_COEF_PIXEL_MAJOR>(a, o);
+    case 16: return planar ? launch_direct_n<16, T, RTI_COEF_PLANAR>(a, o) : launch_direct_n<16, T, RTI_COEF_PIXEL_MAJOR>(a, o);
+    default: return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: k=%d", a.k);
+  }
+}
+
 template <int K, typename T>
 void launch_lane_t(const PmArgs& a) {
   const dim3 grid(grid_1d(a.P, 256), a.C);
@@ -875,6 +1039,8 @@ extern "C" int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int
   const int64_t cs = channel_stride ? channel_stride : P * ps;
   if (!pm_dma_shape(k, N, in_dtype, P, C, ps, cs) || (kernel & 0xff) == RTI_KERNEL_VALU) return 0;
   const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  if ((kernel & 0xff) == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE) && N % 4 == 0 && pm_direct_ns(N))
+    return RTI_PM_DIRECT * 100000000 + pm_direct_ns(N) * 1000 + (w_req ? w_req : PM_DIRECT_WPC);
   if ((kernel & 0xff) == RTI_KERNEL_AUTO) {
     const VPlan vp = vstream_plan(k, N, 4, w_req);
     if (vp.W && (int64_t)C * P * k * 4 < 0xFFFFFFF0ll) return RTI_PM_VALU_STREAM * 100000000 + (vp.ring >> 10) * 1000 + vp.W;
@@ -922,6 +1088,15 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
                       rti_fit_shared_pm_plan(k, N, in_dtype, P, C, a.ps, a.cs, kernel) != 0 &&
                       aligned_to(I, 16) && aligned_to(coef, 16) && a.ocs % 4 == 0;
   const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  if (dma_ok && sel == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE) && N % 4 == 0 && pm_direct_ns(N)) {
+    DirectOpts o;  // no LDS: straight to registers.  Measurement flags: TILE_WAVES(w) waves per CU,
+    if (w_req) o.wpc = w_req;  // CHUNKS(n) launch generations, ROTATE contiguous runs, PINV_LDS plain loads
+    if (c_req) o.gens = c_req;
+    o.contig = (kernel & RTI_KERNEL_ROTATE) != 0;
+    o.nt = (kernel & RTI_KERNEL_PINV_LDS) == 0;
+    const int st = in_dtype == RTI_F32 ? launch_direct<float>(a, o) : launch_direct<int32_t>(a, o);
+    return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
+  }
   if (dma_ok && sel == RTI_KERNEL_AUTO) {  // k <= 9: one pixel per lane, packed FMAs
     const VPlan vp = vstream_plan(k, N, es, w_req);
     if (vp.W && vstream_coef_ok(a)) {

@@ -361,7 +361,7 @@ rbf_solve_gji(const float* __restrict__ lu, const float* __restrict__ lv, const 
   }
   if (singular && t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
   const bool again = !singular && (lost || !conv);  // block-uniform
-  if (again && t == 0) redo[p] = 1;
+  if (again && t == 0) redo[1 + atomicAdd(redo, 1)] = (int)p;  // the fp64 fallback's list
   if (t < N) wT[(int64_t)t * P + p] = (singular || again) ? __builtin_nan("") : w_t;
 }
 
@@ -618,7 +618,7 @@ rbf_solve_gjs(const float* __restrict__ lu, const float* __restrict__ lv, const 
   }
   if (singular && t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
   const bool again = !singular && (lost || !conv);  // block-uniform
-  if (again && t == 0) redo[p] = 1;
+  if (again && t == 0) redo[1 + atomicAdd(redo, 1)] = (int)p;  // the fp64 fallback's list
   if (t < N) wT[(int64_t)t * P + p] = (singular || again) ? __builtin_nan("") : w_t;
 }
 
@@ -802,42 +802,40 @@ rbf_eval(const double* __restrict__ wT, const float2* __restrict__ xyT, int N, i
 }
 
 // ---- fp64 fallback for the pixels the fp32 inverse cannot take ------------------------------------
-// rbf_solve_gji / rbf_solve_gjs flag a pixel (redo[p] = 1) when a Gauss-Jordan pivot of S is not
-// positive in fp32 or the refinement does not reach the fp64 floor — cond(A) ≳ 1e8, i.e. nearly
-// repeated light directions, where SciPy's fp64 LU still returns a solution.  This kernel solves
-// exactly those pixels the way SciPy does: fp64 Gauss-Jordan with partial pivoting on [A | b], the
-// matrix in a per-workgroup global workspace (N·(N+1) doubles, L2/MALL-resident), rows never swapped
-// (a used-row mask; the pivot of step k is the largest |a_ik| among unused rows, ties to the lower
-// row), the system left diagonal, w at node k = b_p / a_pk of step k's pivot row p.  A fixed grid of
-// workgroups strides over the pixels 256 at a time (one flag load per thread, the flagged pixels
-// listed in LDS), so a launch without flagged pixels costs one coalesced pass over the flags.
-// The grid is one workgroup per CU (device_cus(), 256 on MI355X); each holds one N·(N+1) fp64 slot.
+// rbf_solve_gji / rbf_solve_gjs list a pixel (redo[0] = count, redo[1 ..] = pixels) when a Gauss-Jordan
+// pivot of S is not positive in fp32 or the refinement does not reach the fp64 floor — cond(A) ≳ 1e8:
+// nearly repeated light directions.  With per-pixel directions that happens wherever the line through two
+// light positions meets the ROI plane (the two directions coincide there), so a few pixels of a real
+// capture need it (c8: 8 of 160 000) and SciPy's fp64 LU still returns a solution for them.  This kernel
+// solves exactly those pixels the way SciPy does: fp64 Gauss-Jordan with partial pivoting on [A | b], rows
+// never swapped (a used-row mask; the pivot of step k is the largest |a_ik| among unused rows, ties to the
+// lower row), the system left diagonal, w at node k = b_p / a_pk of step k's pivot row p.  The listed pixels
+// are spread over the grid (workgroup b takes list entries b, b + G, ...: one pixel per CU for a handful of
+// them), and [A | b] lives in LDS up to N = RBF_FB_LDS_N (else in a per-workgroup global slot), eliminated
+// by a 16 × 16 thread grid (rows × columns).  A launch with an empty list reads one int.
 constexpr int RBF_FB_THREADS = 256;
+constexpr size_t RBF_FB_LDS = 152 * 1024;  // dynamic LDS for [A | b] (the static part is ≈ 7.3 KiB)
+__host__ __device__ constexpr bool fb_in_lds(int N) { return (size_t)N * (N + 1) * sizeof(double) <= RBF_FB_LDS; }
+constexpr int RBF_FB_LDS_N = 138;
+static_assert(fb_in_lds(RBF_FB_LDS_N) && !fb_in_lds(RBF_FB_LDS_N + 1), "RBF_FB_LDS_N");
 
-template <typename T>
+template <typename T, bool LDSM>
 __global__ void __launch_bounds__(RBF_FB_THREADS)
 rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
-               const int* __restrict__ redo, double* __restrict__ ws, double* __restrict__ wT,
+               const int* __restrict__ list, double* __restrict__ ws, double* __restrict__ wT,
                int* __restrict__ status, int* __restrict__ fallback_px) {
+  extern __shared__ double ldsM[];
   __shared__ double xs[RBF_MAX_N], ys[RBF_MAX_N], lf[RBF_MAX_N];
   __shared__ int used[RBF_MAX_N];
   __shared__ double s_val[RBF_FB_THREADS / 64];
   __shared__ int s_row[RBF_FB_THREADS / 64];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  __shared__ int64_t s_list[RBF_FB_THREADS];
-  __shared__ int s_count;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, tx = t & 15, ty = t >> 4;
   const int ld = N + 1;
-  double* M = ws + (int64_t)blockIdx.x * N * ld;  // [N][N + 1]: A | b
-  // the flags of 256 pixels per pass are read in parallel and the flagged ones listed in LDS
-  for (int64_t first = (int64_t)blockIdx.x * RBF_FB_THREADS; first < P; first += (int64_t)gridDim.x * RBF_FB_THREADS) {
-  if (t == 0) s_count = 0;
-  __syncthreads();
-  if (first + t < P && redo[first + t]) s_list[atomicAdd(&s_count, 1)] = first + t;
-  __syncthreads();
-  const int count = s_count;
-  if (t == 0 && count > 0 && fallback_px) atomicAdd(fallback_px, count);  // (reported by rti_rbf_perpixel_ex)
-  for (int li = 0; li < count; ++li) {
-    const int64_t p = s_list[li];
+  double* M = LDSM ? ldsM : ws + (int64_t)blockIdx.x * N * ld;  // [N][N + 1]: A | b
+  const int count = list[0];
+  if (blockIdx.x == 0 && t == 0 && count > 0 && fallback_px) atomicAdd(fallback_px, count);  // (rti_rbf_perpixel_ex)
+  for (int li = blockIdx.x; li < count; li += gridDim.x) {
+    const int64_t p = list[1 + li];
     const int64_t base = p * N;
     for (int j = t; j < N; j += RBF_FB_THREADS) xs[j] = (double)lu[base + j], ys[j] = (double)lv[base + j], used[j] = 0;
     __syncthreads();
@@ -875,11 +873,13 @@ rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const
       const double piv = M[(int64_t)row * ld + k];
       for (int i = t; i < N; i += RBF_FB_THREADS) lf[i] = i == row ? 0.0 : M[(int64_t)i * ld + k] / piv;
       __syncthreads();
-      // eliminate column k from every other row (Gauss-Jordan): columns k+1 .. N across the threads
+      // eliminate column k from every other row (Gauss-Jordan): rows over ty, columns k+1 .. N over tx
       const double* prow = M + (int64_t)row * ld;
-      for (int j = k + 1 + t; j <= N; j += RBF_FB_THREADS) {
-        const double pj = prow[j];
-        for (int i = 0; i < N; ++i) M[(int64_t)i * ld + j] = fma(-lf[i], pj, M[(int64_t)i * ld + j]);
+      for (int i = ty; i < N; i += RBF_FB_THREADS / 16) {
+        if (i == row) continue;
+        const double f = lf[i];
+        double* mi = M + (int64_t)i * ld;
+        for (int j = k + 1 + tx; j <= N; j += 16) mi[j] = fma(-f, prow[j], mi[j]);
       }
       if (t == 0) used[row] = k + 1;  // step of this pivot row, + 1
       __syncthreads();
@@ -893,9 +893,7 @@ rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const
         wT[(int64_t)k * P + p] = M[(int64_t)i * ld + N] / M[(int64_t)i * ld + k];
       }
     }
-    __syncthreads();  // xs / used / M are reused by the next flagged pixel
-  }
-  __syncthreads();  // s_list / s_count are reused by the next pass
+    __syncthreads();  // xs / used / M are reused by the next listed pixel
   }
 }
 
@@ -1110,6 +1108,43 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       if constexpr (LL) {
         // left-looking update: pan[r][c] −= Σ_{q < k0} L[k0+r][q]·L[k0+c][q], in chunks of CH_QC columns q;
         // L[k0+c][q] (c < kb) staged in LDS, L[k0+r][q] = LT[q][k0+r] read coalesced by thread r
+        if (rows <= TH) {
+          // one row per thread: its QP values of L for the next chunk are loaded while the current chunk's
+          // FMAs run, and the sums stay in registers across the chunks (one LDS update at the end)
+          constexpr int QP = NB >= 32 ? 8 : 16;  // chunk (<= CH_QC): 2 × QP staged values + NB sums in registers
+          const int r = t;
+          const bool act = r < rows;
+          double acc[NB], li[QP];
+#pragma unroll
+          for (int c = 0; c < NB; ++c) acc[c] = 0.0;
+          auto fetch = [&](int qb) {
+            const double* lcol = M + (int64_t)qb * ld + k0 + r;
+#pragma unroll
+            for (int u = 0; u < QP; ++u) li[u] = (act && qb + u < k0) ? lcol[(int64_t)u * ld] : 0.0;
+          };
+          if (k0 > 0) fetch(0);
+          for (int qb = 0; qb < k0; qb += QP) {
+            for (int idx = t; idx < QP * NB; idx += TH) {  // (rows past the chunk zero: 0·stale could be NaN)
+              const int q = idx / NB, c = idx - q * NB;
+              bq[idx] = (c < kb && qb + q < k0) ? M[(int64_t)(qb + q) * ld + k0 + c] : 0.0;
+            }
+            __syncthreads();
+            double cur[QP];
+#pragma unroll
+            for (int u = 0; u < QP; ++u) cur[u] = li[u];
+            if (qb + QP < k0) fetch(qb + QP);
+#pragma unroll
+            for (int u = 0; u < QP; ++u)
+#pragma unroll
+              for (int c = 0; c < NB; ++c) acc[c] = fma(cur[u], bq[u * NB + c], acc[c]);
+            __syncthreads();  // bq is restaged
+          }
+          if (act)
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+              if (c < kb && (r >= kb || c <= r)) pan[r * LDP + c] -= acc[c];
+          __syncthreads();
+        } else
         for (int qb = 0; qb < k0; qb += CH_QC) {
           const int qc = min(CH_QC, k0 - qb);
           for (int idx = t; idx < qc * NB; idx += TH) {
@@ -1383,7 +1418,7 @@ int gji_refine() {
 
 bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); }
 
-// redo / fb_ws: the flag per pixel (zeroed) and the fp64 fallback's workspace, when uses_gji(N)
+// redo / fb_ws: the fallback's pixel list (redo[0] = count, zeroed) and its workspace, when uses_gji(N)
 template <typename T>
 void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
                   int* status, int* redo, double* fb_ws, int64_t chol_grid, int64_t fb_grid, int* fallback_px,
@@ -1430,8 +1465,16 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
       hipLaunchKernelGGL((rbf_solve_gji<32, T>), g, dim3(1024), 0, s, lu, lv, In, N, P, wT, xyT, status, redo,
                          gji_refine());
     const unsigned fg = (unsigned)(P < fb_grid ? P : fb_grid);
-    hipLaunchKernelGGL((rbf_solve_fp64<T>), dim3(fg), dim3(RBF_FB_THREADS), 0, s, lu, lv, In, N, P, redo, fb_ws, wT,
-                       status, fallback_px);
+    if (fb_in_lds(N)) {
+      const size_t mb = (size_t)N * (N + 1) * sizeof(double);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rbf_solve_fp64<T, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)mb);
+      hipLaunchKernelGGL((rbf_solve_fp64<T, true>), dim3(fg), dim3(RBF_FB_THREADS), mb, s, lu, lv, In, N, P, redo,
+                         fb_ws, wT, status, fallback_px);
+    } else {
+      hipLaunchKernelGGL((rbf_solve_fp64<T, false>), dim3(fg), dim3(RBF_FB_THREADS), 0, s, lu, lv, In, N, P, redo,
+                         fb_ws, wT, status, fallback_px);
+    }
     return;
   }
 #define RBF_GJ(NM)                                                                                       \
@@ -1495,14 +1538,14 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   hipStream_t s = (hipStream_t)stream;
   // workspace: per-pixel weights and nodes, node-major ([N][P]) for the coalesced evaluation
   void* ws = nullptr;
-  // + for the block solvers: a redo flag per pixel and the fp64 fallback's per-workgroup matrices
+  // + for the block solvers: the fp64 fallback's pixel list and (N > RBF_FB_LDS_N) per-workgroup matrices
   const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
   const int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
   const int64_t fb_grid = fb ? (P < device_cus() ? P : device_cus()) : 0;
-  const size_t fb_ws_bytes = fb ? (size_t)fb_grid * N * (N + 1) * sizeof(double)
+  const size_t fb_ws_bytes = fb ? (fb_in_lds(N) ? 0 : (size_t)fb_grid * N * (N + 1) * sizeof(double))
                                 : (chol ? (size_t)chol_grid * chol_slot_doubles(N) * sizeof(double) : 0);
-  const size_t flag_bytes = fb ? ((size_t)P * sizeof(int) + 255) / 256 * 256 : 0;
+  const size_t flag_bytes = fb ? ((size_t)(P + 1) * sizeof(int) + 255) / 256 * 256 : 0;  // count + pixel list
   const size_t bytes = (size_t)N * P * (sizeof(double) + sizeof(float2)) + fb_ws_bytes + flag_bytes;
   if (hipMallocAsync(&ws, bytes, s) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_rbf_perpixel: workspace allocation of %zu bytes failed", bytes);
@@ -1510,9 +1553,9 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   float2* xyT = reinterpret_cast<float2*>(wT + (size_t)N * P);
   double* fb_ws = reinterpret_cast<double*>(xyT + (size_t)N * P);
   int* redo = reinterpret_cast<int*>(reinterpret_cast<char*>(fb_ws) + fb_ws_bytes);
-  if (fb && hipMemsetAsync(redo, 0, (size_t)P * sizeof(int), s) != hipSuccess) {
+  if (fb && hipMemsetAsync(redo, 0, sizeof(int), s) != hipSuccess) {
     (void)hipFreeAsync(ws, s);
-    return fail(RTI_ERR_HIP, "rti_rbf_perpixel: clearing the redo flags failed");
+    return fail(RTI_ERR_HIP, "rti_rbf_perpixel: clearing the fallback count failed");
   }
   switch (in_dtype) {
     case RTI_F32: launch_solve<float>(lu, lv, I, N, P, wT, xyT, status, redo, fb_ws, chol_grid, fb_grid, fallback_px, s); break;

@@ -47,6 +47,7 @@ RTI_KERNEL_ROTATE = 0x10000000  # measurement variant: per-wave rotated light or
 RTI_PM_VALU_STREAM = 1  # rti_fit_shared_pm_plan forms (include/rti.h)
 RTI_PM_MFMA_STREAM = 2
 RTI_PM_BLOCK = 3
+RTI_PM_DIRECT = 4
 RTI_KERNEL_ONE_LAUNCH = 0x20000000  # measurement variant: AUTO without launch generations
 RTI_KERNEL_ROUNDS = 0x40000000  # measurement variant: AUTO generations as rounds of one launch
 RTI_KERNEL_CHUNKS_SHIFT = 12  # VALU chunks per lane in bits 12-15 (0 = AUTO)

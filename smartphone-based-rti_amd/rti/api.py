@@ -742,12 +742,13 @@ def interpolate_rbf(I, lu, lv, qu, qv, out_dtype=torch.float32):
     return apply_operator(rbf_operator(lu, lv, qu, qv), I, out_dtype=out_dtype)
 
 
-def interpolate_rbf_perpixel(I, lu, lv, qu, qv, out_dtype=torch.float64, out_layout="pixel"):
+def interpolate_rbf_perpixel(I, lu, lv, qu, qv, out_dtype=torch.float64, out_layout="pixel", stats=None):
     """Per-pixel linear RBF (the reference's default with per-pixel light lists) on the GPU.
 
     I, lu, lv: pixel-major [.., N] (compute_intensities' layout), on any device.
     Returns [.., E] (out_layout="pixel") or [E, ..] ("eval").  Raises
-    numpy.linalg.LinAlgError if any pixel's system is singular, as SciPy does."""
+    numpy.linalg.LinAlgError if any pixel's system is singular, as SciPy does.
+    stats: a dict receives "fallback_px", the pixels (81 <= N <= 256) re-solved by the fp64 fallback."""
     _require_cuda(I, "I")
     dev = I.device
     odt = _OUT_DTYPES.get(out_dtype)
@@ -767,9 +768,12 @@ def interpolate_rbf_perpixel(I, lu, lv, qu, qv, out_dtype=torch.float64, out_lay
     out = torch.empty(spatial + (E,) if ol == L.RTI_OUT_PIXEL_MAJOR else (E,) + spatial, dtype=out_dtype, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     Ic = I.contiguous()
-    st = L.lib().rti_rbf_perpixel(_vp(lu_d), _vp(lv_d), _vp(Ic), _IN_DTYPES[Ic.dtype], N, P, _vp(luv), E, _vp(out),
-                                  odt, ol, _vp(status), _stream_of(I))
+    fb = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = L.lib().rti_rbf_perpixel_ex(_vp(lu_d), _vp(lv_d), _vp(Ic), _IN_DTYPES[Ic.dtype], N, P, _vp(luv), E,
+                                     _vp(out), odt, ol, _vp(status), _vp(fb), _stream_of(I))
     L.check(st, "rti_rbf_perpixel")
+    if stats is not None:
+        stats["fallback_px"] = int(fb.item())
     if int(status.item()) == L.RTI_ERR_SINGULAR:
         raise np.linalg.LinAlgError("Matrix is singular.")
     return out

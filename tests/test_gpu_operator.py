@@ -249,10 +249,34 @@ def test_rbf_perpixel_near_repeated_nodes_fp64_fallback(cuda, n, d):
     lu[2, 7], lv[2, 7] = np.float32(lu[2, 3] + d), lv[2, 3]
     inten = rng.integers(0, 256, (4, n)).astype(np.int32)
     qu, qv = rng.uniform(-1, 1, 200), rng.uniform(-1, 1, 200)
-    out = rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv).cpu().numpy()
+    stats = {}
+    out = rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv, stats=stats).cpu().numpy()
+    assert stats["fallback_px"] <= 1  # only the perturbed pixel may need it (N > 256: the Cholesky, no fallback)
     for p in range(4):
         ref = o.rbf_linear(lu[p], lv[p], inten[p], qu, qv)
         err, ok = relight_close(out[p], ref, rtol=1e-7 if p == 2 else 1e-8)
+        assert ok, (p, err)
+
+
+@pytest.mark.parametrize("n", [100, 138, 139, 200])
+def test_rbf_perpixel_fallback_many_pixels(cuda, n):
+    """Every pixel of the launch nearly repeats a light direction: all of them go to the fp64 fallback,
+    whose list spreads them over the grid (more pixels than workgroups: each takes several), with [A | b]
+    in LDS up to N = 138 and in a global slot above; the count comes back as stats["fallback_px"]."""
+    P = 300
+    rng = np.random.default_rng(n + 1)
+    ys, xs = np.divmod(np.arange(P), 20)
+    cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
+    lu, lv = o.light_dirs_for_pixels(cams, xs, ys)
+    lu[:, 7], lv[:, 7] = lu[:, 3] + np.float32(1e-6), lv[:, 3]
+    inten = rng.integers(0, 256, (P, n)).astype(np.int32)
+    qu, qv = rng.uniform(-1, 1, 64), rng.uniform(-1, 1, 64)
+    stats = {}
+    out = rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv, stats=stats).cpu().numpy()
+    assert stats["fallback_px"] == P
+    for p in list(range(0, P, 37)) + [P - 1]:
+        ref = o.rbf_linear(lu[p], lv[p], inten[p], qu, qv)
+        err, ok = relight_close(out[p], ref, rtol=1e-7)
         assert ok, (p, err)
 
 

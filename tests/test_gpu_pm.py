@@ -20,13 +20,21 @@ def test_golden_256x256_N20_pixel_major(cuda):
     d = golden("ptm_shared_256x256_N20.npz")
     Ipm = torch.as_tensor(np.ascontiguousarray(np.moveaxis(d["I"], 0, -1))).to(cuda, torch.float32)  # [256, 256, 20]
     plan = L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, 0)
-    assert plan // 10**8 == L.RTI_PM_VALU_STREAM, plan  # AUTO for PTM-6: the packed-FMA stream
+    assert plan // 10**8 == L.RTI_PM_DIRECT, plan  # AUTO (N % 4 == 0): straight to registers
+    plan = L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, L.RTI_KERNEL_STAGE)
+    assert plan // 10**8 == L.RTI_PM_VALU_STREAM, plan  # AUTO through the LDS ring: the packed-FMA stream
     for layout in ("pixel", "planar"):
         coef = rti.fit(Ipm, d["lu"], d["lv"], stack="pixel", layout=layout).cpu().numpy()
         if layout == "planar":
             coef = np.moveaxis(coef, 0, -1)
         err, ok = coef_close(coef, d["coef"])
         assert ok, (layout, err)
+        got = torch.empty((256 * 256, 6) if layout == "pixel" else (6, 256 * 256), device=cuda)
+        pv = torch.as_tensor(rti.pinv(d["lu"], d["lv"], "ptm").astype(np.float32), device=cuda)
+        rti.api.fit_shared_pm_into(pv, Ipm.reshape(-1, 20), got, k=6, layout=layout, flags=L.RTI_KERNEL_STAGE)
+        got = got.cpu().numpy() if layout == "pixel" else got.T.cpu().numpy()
+        err, ok = coef_close(got.reshape(256, 256, 6), d["coef"])
+        assert ok, ("stage", layout, err)
     # a light-major-shaped VIEW of the pixel-major stack goes to the same kernel without a copy
     view = Ipm.permute(2, 0, 1)
     assert not view.is_contiguous()
@@ -44,10 +52,11 @@ def _ref(I_cpn, pinv64):
 
 
 @pytest.mark.parametrize("basis", ["ptm", "hsh9", "hsh"])
-@pytest.mark.parametrize("N", [16, 17, 18, 20, 50, 100, 150, 200, 256])
+@pytest.mark.parametrize("N", [16, 17, 18, 20, 36, 50, 64, 100, 112, 128, 150, 200, 208, 252, 256, 260])
 @pytest.mark.parametrize("in_dtype", [torch.float32, torch.int32, torch.uint8])
 def test_pm_shapes_vs_fp64(cuda, basis, N, in_dtype):
-    """Every light-count class (N % 16 partial chunks, N % 4 in {0, 1, 2}: b128 / b64 / b32 LDS reads),
+    """Every light-count class (N % 16 partial chunks, N % 4 in {0, 1, 2}: b128 / b64 / b32 LDS reads; the
+    direct form's 16-light step buckets 2/4/7/8/13/16 at and between their edges, and N = 260 past them),
     pixel counts around block multiples (a partial last block), two channels, both coefficient layouts,
     fp32 / int32 stacks (DMA + MFMA) and uint8 (one lane per pixel)."""
     k = rti.basis_terms(basis)
@@ -78,7 +87,8 @@ def test_pm_shapes_vs_fp64(cuda, basis, N, in_dtype):
                                       ("tile", 4, 3), ("mfma", 0, 1), ("mfma", 0, 2), ("mfma", 0, 3), ("mfma", 0, 4),
                                       ("mfma", 0, 6), ("mfma", 0, 8), ("mfma_contig", 0, 8), ("mfma_contig", 0, 3),
                                       ("mfma", 2, 8), ("mfma", 3, 4), ("mfma_contig", 2, 6),
-                                      ("auto", 0, 4), ("auto", 0, 3), ("auto", 0, 2), ("auto", 0, 1)])
+                                      ("auto", 0, 4), ("auto", 0, 3), ("auto", 0, 2), ("auto", 0, 1),
+                                      ("auto", 0, 12), ("auto", 0, 8), ("auto_stage", 0, 4), ("auto_stage", 0, 2)])
 @pytest.mark.parametrize("N", [20, 100, 33, 200])
 def test_pm_block_plans(cuda, kern, g, w, N):
     """kernel="tile" (the double-buffered block form): RTI_KERNEL_CHUNKS(G) / TILE_WAVES(W) = 16, 32 and
@@ -93,6 +103,8 @@ def test_pm_block_plans(cuda, kern, g, w, N):
     flags = (g << L.RTI_KERNEL_CHUNKS_SHIFT) | (w << L.RTI_KERNEL_TILE_WAVES_SHIFT)
     if kern == "mfma_contig":  # each wave one contiguous run of units instead of interleaved units
         kern, flags = "mfma", flags | L.RTI_KERNEL_ROTATE
+    if kern == "auto_stage":  # AUTO through the LDS ring (the VALU stream); plain AUTO: direct, W waves per CU
+        kern, flags = "auto", flags | L.RTI_KERNEL_STAGE
     if not L.lib().rti_fit_shared_pm_plan(k, N, L.RTI_F32, P, 3, 0, 0, flags | rti.api._KERNELS[kern]):
         pytest.skip("plan does not fit the LDS")
     rng = np.random.default_rng(g * 10 + w + N)
@@ -134,18 +146,21 @@ def test_pm_lane_fallback(cuda):
                                    kernel="mfma")
 
 
-def test_pm_nan_stays_in_its_pixel(cuda):
+@pytest.mark.parametrize("N,flags", [(21, 0), (20, 0), (20, L.RTI_KERNEL_STAGE), (100, 0), (104, 0)])
+def test_pm_nan_stays_in_its_pixel(cuda, N, flags):
     """A NaN intensity makes its own pixel's coefficients NaN (0·NaN in the reference's matmul) and no
-    other pixel's: the masked tail chunk reads the next pixel's values and must not leak them."""
-    N, P = 21, 64
+    other pixel's: the masked tail chunk (LDS forms) and the out-of-range lights of the last 16-light step
+    (direct form) must not bring in the next pixel's values."""
+    P = 64
     lu, lv = o.synth_dirs(N, 2)
     pv = torch.as_tensor(rti.pinv(lu, lv, "ptm").astype(np.float32), device=cuda)
     I = torch.full((P, N), 7.0, device=cuda)
     I[5, 0] = float("nan")
     I[6, 0] = float("inf")
-    coef = rti.api.fit_shared_pm_into(pv, I, torch.empty((P, 6), device=cuda), k=6).cpu().numpy()
+    I[40, N - 1] = float("nan")
+    coef = rti.api.fit_shared_pm_into(pv, I, torch.empty((P, 6), device=cuda), k=6, flags=flags).cpu().numpy()
     bad = ~np.isfinite(coef).all(-1)
-    assert bad[5] and bad[6] and bad.sum() == 2
+    assert bad[5] and bad[6] and bad[40] and bad.sum() == 3
 
 
 @pytest.mark.slow

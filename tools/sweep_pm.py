@@ -64,18 +64,27 @@ def main():
         if plan:
             variants.append((f"pm_block_{plan % 100000000 // 1000}px_w{plan % 1000}",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="tile", flags=fl)))
+    direct = [(f"pm_direct_{w}wpc", w << L.RTI_KERNEL_TILE_WAVES_SHIFT) for w in (4, 8, 12)]
+    direct += [(f"pm_direct_gens{g}", g << L.RTI_KERNEL_CHUNKS_SHIFT) for g in (2, 4, 6)]
+    direct += [("pm_direct_contig", L.RTI_KERNEL_ROTATE), ("pm_direct_plain_loads", L.RTI_KERNEL_PINV_LDS),
+               ("pm_direct_contig_gens4", L.RTI_KERNEL_ROTATE | (4 << L.RTI_KERNEL_CHUNKS_SHIFT))]
+    for name, fl in direct:
+        plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
+        if plan // 100000000 == L.RTI_PM_DIRECT:
+            variants.append((name, lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
     for w in (4, 3, 2):
-        fl = w << L.RTI_KERNEL_TILE_WAVES_SHIFT
+        fl = (w << L.RTI_KERNEL_TILE_WAVES_SHIFT) | L.RTI_KERNEL_STAGE
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
         if plan // 100000000 == L.RTI_PM_VALU_STREAM:
             variants.append((f"pm_valu_w{w}_ring{plan % 100000000 // 1000}K",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
     variants.append(("pm_auto", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto")))
     if k <= 9:  # measurement variants of the VALU stream: no stores / no arithmetic
+        st = L.RTI_KERNEL_STAGE
         variants.append(("pm_valu_nostores", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
-                                                                              flags=L.RTI_KERNEL_ONE_LAUNCH)))
+                                                                              flags=st | L.RTI_KERNEL_ONE_LAUNCH)))
         variants.append(("pm_valu_noarith", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
-                                                                             flags=L.RTI_KERNEL_ROUNDS)))
+                                                                             flags=st | L.RTI_KERNEL_ROUNDS)))
     agree = {}
     for name, fn in variants:
         for _ in range(3):
