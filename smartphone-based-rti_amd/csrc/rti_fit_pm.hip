@@ -593,40 +593,40 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
   }
 }
 
-// DIRECT form (AUTO for N % 4 == 0, N <= 256): no LDS at all.  A wave streams 16-pixel groups (16·N
-// contiguous values) straight into VGPRs: for 16-light step s, lane (q, r) loads I[p0 + q][16s + 4r .. +3]
-// with one 16-byte buffer load, which is the B operand of four v_mfma_f32_16x16x4_f32 (MFMA j takes element
-// j: light 16s + 4r + j at k-index r, 16 pixels × 64 contiguous bytes per load instruction); the A operand,
-// pinv[q][16s + 4r + j], stays in VGPRs for the whole launch (4·NS values per lane).  D groups of loads are
-// in flight per wave.  Waves take groups gw, gw + GW, ... over the flattened (channel, group) space, so the
-// grid sweeps the stack as one contiguous window.  Lights past N and pixels past P are out-of-range buffer
-// offsets (they read zero and move no bytes), so no lane reads a neighbour pixel's values (a NaN stays in
-// its pixel).  The loads and MFMAs are plain straight-line code per group, so the compiler's own vmcnt
-// waits are exact: a group waits for its own loads only, with the next D − 1 groups' loads and the
-// previous groups' stores still in flight.
-// AUX: the loads' cache policy (2 = non-temporal: the stack is read once; 0 = plain, a measurement variant)
-template <int K, typename T, int LAYOUT, int NS, int D, int AUX = 2>
+// DIRECT form (AUTO for N % 4 == 0, N <= 256): the stack goes straight into VGPRs, LDS only stages the
+// coefficients.  A wave streams 16-pixel groups (16·N contiguous values): for 16-light step s, lane (q, r)
+// loads I[p0 + q][16s + 4r .. +3] with one 16-byte buffer load, which is the B operand of four
+// v_mfma_f32_16x16x4_f32 (MFMA j takes element j: light 16s + 4r + j at k-index r, 16 pixels × 64 contiguous
+// bytes per load instruction); the A operand, pinv[q][16s + 4r + j], stays in VGPRs for the whole launch
+// (4·NS values per lane).  D groups of loads are in flight per wave.  Lights past N and pixels past P are
+// out-of-range buffer offsets (they read zero and move no bytes), so no lane reads a neighbour pixel's values
+// (a NaN stays in its pixel).  Loads are plain, not non-temporal: a load instruction touches each 128-byte
+// line of its 16 rows by halves, and non-temporal halves went to HBM twice (c3 0.93 against 0.69 ms).
+// Runs: a wave takes RUN consecutive groups (runs interleaved over the waves of the grid), parks each group's
+// coefficients in its LDS run buffer and writes the run out as one burst of 1-KiB stores (pixel-major: the
+// run's coefficients are one contiguous range).  Stores spread thinly through the read stream cost the most
+// (the mixed read/write probes, DESIGN §4.1e: 0.61 against 0.52 ms for the same bytes written in bursts);
+// the loads of the next D groups stay in flight across a burst.  The loads and MFMAs are straight-line code
+// per group, so the compiler's own vmcnt waits are exact.
+template <int K, int NS>
+constexpr int pm_direct_run() { return K > 9 ? 12 : 24; }  // groups per run (a multiple of the depth)
+
+template <int K, typename T, int LAYOUT, int NS, int D>
 __global__ void __launch_bounds__(256)
 fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
-              float* __restrict__ coef, int64_t ocstride, int ngrp, int g0, int tg, int contig) {
+              float* __restrict__ coef, int64_t ocstride, int ngrp, int nrun, int r0, int tr) {
+  constexpr int RUN = pm_direct_run<K, NS>(), RPX = 16 * RUN;  // groups and pixels per run
+  static_assert(RUN % D == 0, "runs of whole pipeline steps");
   typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) float runbuf[];  // per wave: RPX·K floats
   const int lane = threadIdx.x & 63, q = lane & 15, r = lane >> 4;
   const int W = blockDim.x >> 6;
-  const int gw = (int)blockIdx.x * W + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), GW = (int)gridDim.x * W;
-  // this wave's groups of [g0, g0 + tg): gw, gw + GW, ... (interleaved) or one run of ⌈tg / GW⌉ (contig)
-  int first, step, ni;
-  if (contig) {
-    const int per = (tg + GW - 1) / GW;
-    first = gw * per;
-    step = 1;
-    ni = tg - first < per ? tg - first : per;
-  } else {
-    first = gw;
-    step = GW;
-    ni = gw < tg ? (tg - 1 - gw) / GW + 1 : 0;
-  }
-  if (ni <= 0) return;
-  first += g0;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gw = (int)blockIdx.x * W + wave, GW = (int)gridDim.x * W;
+  // this wave's runs of [r0, r0 + tr): gw, gw + GW, ...; run index = channel·nrun + run in channel
+  const int nr = gw < tr ? (tr - 1 - gw) / GW + 1 : 0;
+  if (nr == 0) return;
+  float* __restrict__ buf = runbuf + wave * RPX * K;
   float w[NS][4];
   int off[NS];
 #pragma unroll
@@ -636,28 +636,29 @@ fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
     for (int j = 0; j < 4; ++j) w[s][j] = (q < K && n + j < N) ? pinv[q * N + n + j] : 0.f;
     off[s] = n < N ? (q * N + n) * (int)sizeof(T) : (int)PM_OOB;
   }
-  const int gq = step / ngrp, gr = step - gq * ngrp;  // advance of a group cursor by one step
-  const int cbytes = (int)(P * K * 4);
-  // load cursor (the group D ahead) and store cursor (the group computed)
-  int lc = first / ngrp, lg = first - lc * ngrp, li = 0;
-  int sc = lc, sg = lg;
-  auto advance = [&](int& c, int& g) {
-    c += gq;
-    g += gr;
-    if (g >= ngrp) {
-      g -= ngrp;
-      ++c;
-    }
-  };
+  const int gq = GW / nrun, gr = GW - gq * nrun;  // advance of a run cursor by GW runs
+  const int first = r0 + gw;
+  // load cursor (D groups ahead of the compute): run (lc, lj), group lw inside it, runs left lrl
+  int lc = first / nrun, lj = first - lc * nrun, lw = 0, lrl = nr;
+  int sc = lc, sj = lj;  // the run being computed
   auto load = [&](u4 (&x)[NS]) {
-    const int64_t p0 = (int64_t)lg * 16;
-    const int rows = li < ni ? (int)(P - p0 < 16 ? P - p0 : 16) : 0;  // 0: past the stream, zero-traffic loads
+    const int g = lj * RUN + lw;  // group in the channel
+    const int64_t p0 = (int64_t)g * 16;
+    const int rows = (lrl > 0 && g < ngrp) ? (int)(P - p0 < 16 ? P - p0 : 16) : 0;  // 0: zero-traffic loads
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<T*>(I + (int64_t)lc * cstride + p0 * N), (short)0, rows * N * (int)sizeof(T), 0x00020000);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) x[s] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[s], 0, AUX);
-    ++li;
-    advance(lc, lg);
+    for (int s = 0; s < NS; ++s) x[s] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[s], 0, 0);
+    if (++lw == RUN) {
+      lw = 0;
+      --lrl;
+      lj += gr;
+      lc += gq;
+      if (lj >= nrun) {
+        lj -= nrun;
+        ++lc;
+      }
+    }
   };
   u4 x[D][NS];
 #pragma unroll
@@ -665,27 +666,68 @@ fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
     load(x[d]);
     __builtin_amdgcn_sched_barrier(0);  // the prologue's groups in stream order
   }
-  for (int i = 0; i < ni; i += D) {
+  for (int run = 0; run < nr; ++run) {
+    for (int i = 0; i < RUN; i += D) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      // no exit inside the unrolled groups (the loop runs whole multiples of D; groups past the wave's last
-      // compute zeros and drop their stores): an exit there lets the compiler sink the loads behind it
-      __builtin_amdgcn_sched_barrier(0);
-      floatx4 acc[4];
+      for (int d = 0; d < D; ++d) {
+        __builtin_amdgcn_sched_barrier(0);  // each group's loads in their own place
+        floatx4 acc[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
+        for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[s][j], bits_f<T>(x[d][s][j]), acc[j], 0, 0,
-                                                        0);
-      load(x[d]);
-      const floatx4 c = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef + (int64_t)sc * ocstride, (short)0,
-                                                                          i + d < ni ? cbytes : 0, 0x00020000);
-      store_group<K, LAYOUT>(rs, c, (int64_t)sg * 16 + q, P, r);
-      advance(sc, sg);
+          for (int j = 0; j < 4; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[s][j], bits_f<T>(x[d][s][j]), acc[j], 0, 0, 0);
+        load(x[d]);
+        const floatx4 c = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        // lane (q, r): coefficients 4r .. 4r+3 of pixel (i + d)·16 + q of the run
+        const int px = (i + d) * 16 + q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (4 * r + e < K) {
+            const float v = c[e];
+            buf[LAYOUT == RTI_COEF_PIXEL_MAJOR ? px * K + 4 * r + e : (4 * r + e) * RPX + px] = v;
+          }
+      }
+    }
+    // the run's burst: its coefficients from the LDS buffer, 1 KiB per store instruction (pixel-major)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t px0 = (int64_t)sj * RPX;  // first pixel of the run in its channel
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef + (int64_t)sc * ocstride, (short)0,
+                                                                        (int)(P * K * 4), 0x00020000);
+    if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR) {
+      constexpr int BYTES = RPX * K * 4, NI = (BYTES + 1023) / 1024;
+#pragma unroll
+      for (int n = 0; n < NI; ++n) {
+        const int b = 1024 * n + 16 * lane;  // byte in the run (past P: beyond num_records, dropped)
+        const floatx4 v = b < BYTES ? *reinterpret_cast<const floatx4*>(reinterpret_cast<const char*>(buf) + b)
+                                    : floatx4{0.f, 0.f, 0.f, 0.f};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(intx4, v), rs,
+                                               b < BYTES ? (int)(px0 * K * 4) + b : (int)PM_OOB, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int n = 0; n < RPX / 64; ++n) {
+          const int px = 64 * n + lane;
+          const float v = buf[i * RPX + px];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), rs,
+                                                px0 + px < P ? (int)(((int64_t)i * P + px0 + px) * 4) : (int)PM_OOB,
+                                                0, 0);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the buffer is rewritten by the next run
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    sj += gr;
+    sc += gq;
+    if (sj >= nrun) {
+      sj -= nrun;
+      ++sc;
     }
   }
 }
@@ -951,27 +993,28 @@ constexpr int PM_DIRECT_WPC = 8;  // waves per CU (AUTO)
 
 struct DirectOpts {
   int wpc = PM_DIRECT_WPC;  // waves per CU
-  int gens = 1;             // launch generations (consecutive launches over equal group ranges)
-  int contig = 0;           // each wave one contiguous run of groups instead of interleaved groups
-  int nt = 1;               // non-temporal stack loads
+  int gens = 1;             // launch generations (consecutive launches over equal run ranges)
 };
 
 template <int K, typename T, int LAYOUT, int NS>
 int launch_direct_t(const PmArgs& a, const DirectOpts& o) {
-  constexpr int D = pm_direct_depth(NS);
-  const int64_t ngrp = (a.P + 15) / 16, tg = ngrp * a.C;
-  if (tg >= ((int64_t)1 << 31) - 4096) return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: P too large");
-  const int64_t per = (tg + o.gens - 1) / o.gens;
+  constexpr int D = pm_direct_depth(NS), RPX = 16 * pm_direct_run<K, NS>();
+  const int64_t ngrp = (a.P + 15) / 16, nrun = (a.P + RPX - 1) / RPX, tr = nrun * a.C;
+  if (ngrp >= ((int64_t)1 << 31) - 4096 || a.P * K * 4 >= ((int64_t)1 << 31))
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: P too large");
+  auto kern = fit_pm_direct<K, T, LAYOUT, NS, D>;
+  const size_t lds = (size_t)4 * RPX * K * sizeof(float);  // 4 waves per workgroup
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
+  const int64_t per = (tr + o.gens - 1) / o.gens;
   int launches = 0;
-  for (int64_t g0 = 0; g0 < tg; g0 += per) {
-    const int64_t n = tg - g0 < per ? tg - g0 : per;
+  for (int64_t r0 = 0; r0 < tr; r0 += per) {
+    const int64_t n = tr - r0 < per ? tr - r0 : per;
     const int64_t wgs = (n + 3) / 4, cap = device_cus() * (int64_t)o.wpc / 4;
     const unsigned grid = (unsigned)(wgs < cap ? wgs : (cap > 0 ? cap : 1));
-    auto kern = fit_pm_direct<K, T, LAYOUT, NS, D, 2>;
-    if constexpr (std::is_same<T, float>::value && LAYOUT == RTI_COEF_PIXEL_MAJOR && (NS == 7 || NS == 13))
-      if (!o.nt) kern = fit_pm_direct<K, T, LAYOUT, NS, D, 0>;  // measurement: plain loads (c3 / c4 shapes)
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, a.stream, a.pinv, a.N, static_cast<const T*>(a.I), a.P, a.cs,
-                       a.coef, a.ocs, (int)ngrp, (int)g0, (int)n, o.contig);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, a.stream, a.pinv, a.N, static_cast<const T*>(a.I), a.P,
+                       a.cs, a.coef, a.ocs, (int)ngrp, (int)nrun, (int)r0, (int)n);
     note_launches(++launches);
   }
   return RTI_OK;
@@ -1089,11 +1132,9 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
                       aligned_to(I, 16) && aligned_to(coef, 16) && a.ocs % 4 == 0;
   const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
   if (dma_ok && sel == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE) && N % 4 == 0 && pm_direct_ns(N)) {
-    DirectOpts o;  // no LDS: straight to registers.  Measurement flags: TILE_WAVES(w) waves per CU,
-    if (w_req) o.wpc = w_req;  // CHUNKS(n) launch generations, ROTATE contiguous runs, PINV_LDS plain loads
+    DirectOpts o;  // straight to registers.  Measurement flags: TILE_WAVES(w) waves per CU, CHUNKS(n) launch
+    if (w_req) o.wpc = w_req;  // generations
     if (c_req) o.gens = c_req;
-    o.contig = (kernel & RTI_KERNEL_ROTATE) != 0;
-    o.nt = (kernel & RTI_KERNEL_PINV_LDS) == 0;
     const int st = in_dtype == RTI_F32 ? launch_direct<float>(a, o) : launch_direct<int32_t>(a, o);
     return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
   }

@@ -1109,30 +1109,32 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         // left-looking update: pan[r][c] −= Σ_{q < k0} L[k0+r][q]·L[k0+c][q], in chunks of CH_QC columns q;
         // L[k0+c][q] (c < kb) staged in LDS, L[k0+r][q] = LT[q][k0+r] read coalesced by thread r
         if (rows <= TH) {
-          // one row per thread: its QP values of L for the next chunk are loaded while the current chunk's
-          // FMAs run, and the sums stay in registers across the chunks (one LDS update at the end)
-          constexpr int QP = NB >= 32 ? 8 : 16;  // chunk (<= CH_QC): 2 × QP staged values + NB sums in registers
+          // one row per thread, chunks of QP columns q: the next chunk's L values and its staged L[k0+c][q]
+          // element are loaded into registers while the current chunk's FMAs run; the sums stay in registers
+          // across the chunks (one LDS update at the end)
+          constexpr int QP = NB >= 32 ? 8 : 16;  // (<= CH_QC rows of bq)
           const int r = t;
           const bool act = r < rows;
+          const int nch = (k0 + QP - 1) / QP;
+          const double* lrow = M + k0 + r;  // L[k0+r][q] = LT[q][k0+r]
+          const int bqq = t / NB, bc = t - (t / NB) * NB;  // this thread's staged element (t < QP·NB)
+          const bool bok = t < QP * NB && bc < kb;
           double acc[NB], li[QP];
 #pragma unroll
           for (int c = 0; c < NB; ++c) acc[c] = 0.0;
-          auto fetch = [&](int qb) {
-            const double* lcol = M + (int64_t)qb * ld + k0 + r;
 #pragma unroll
-            for (int u = 0; u < QP; ++u) li[u] = (act && qb + u < k0) ? lcol[(int64_t)u * ld] : 0.0;
-          };
-          if (k0 > 0) fetch(0);
-          for (int qb = 0; qb < k0; qb += QP) {
-            for (int idx = t; idx < QP * NB; idx += TH) {  // (rows past the chunk zero: 0·stale could be NaN)
-              const int q = idx / NB, c = idx - q * NB;
-              bq[idx] = (c < kb && qb + q < k0) ? M[(int64_t)(qb + q) * ld + k0 + c] : 0.0;
-            }
+          for (int u = 0; u < QP; ++u) li[u] = (act && u < k0) ? lrow[(int64_t)u * ld] : 0.0;
+          double bn = (bok && bqq < k0) ? M[(int64_t)bqq * ld + k0 + bc] : 0.0;
+          for (int ch = 0; ch < nch; ++ch) {
+            if (t < QP * NB) bq[t] = bn;  // (zeros past the chunk: 0·stale could be NaN)
             __syncthreads();
             double cur[QP];
 #pragma unroll
             for (int u = 0; u < QP; ++u) cur[u] = li[u];
-            if (qb + QP < k0) fetch(qb + QP);
+            const int nq = (ch + 1) * QP;
+#pragma unroll
+            for (int u = 0; u < QP; ++u) li[u] = (act && nq + u < k0) ? lrow[(int64_t)(nq + u) * ld] : 0.0;
+            bn = (bok && nq + bqq < k0) ? M[(int64_t)(nq + bqq) * ld + k0 + bc] : 0.0;
 #pragma unroll
             for (int u = 0; u < QP; ++u)
 #pragma unroll

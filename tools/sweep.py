@@ -73,6 +73,9 @@ def main():
     plib = os.path.join(ROOT, "tools", "probe", "libhbm_probe.so")
     tlib = os.path.join(ROOT, "tools", "probe", "libtile_probe.so")
     if os.path.exists(tlib) and k == 16 and not args.no_probe:
+        # the probe includes rti_fit.hip and resolves librti's host helpers (rti::fail, ...) from it
+        ctypes.CDLL(os.path.join(ROOT, "smartphone-based-rti_amd", "rti", "librti.so"),
+                    mode=os.RTLD_NOW | os.RTLD_GLOBAL)
         tprobe = ctypes.CDLL(tlib)
         tprobe.probe_tile_nostore.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]

@@ -54,7 +54,7 @@ def main():
         I8 = I.to(torch.uint8)
         i8 = ctypes.c_void_p(I8.data_ptr())
         variants = [("fit_h16_auto", lambda: rti.api.fit_h16_into(h16op, I8, coef, k=k, layout="pixel"))]
-        for nc, launches in ((1, 1), (2, 1), (4, 1), (8, 1), (2, 4), (4, 4), (8, 4)):
+        for nc, launches in ((2, 1), (4, 1), (2, 4), (4, 4)):  # (the probe needs P % (256·nc) == 0, N % (8/nc) == 0)
             for place in (0, 1):
                 variants.append((f"mix_u8_nc{nc}_L{launches}_p{place}",
                                  (lambda nc=nc, launches=launches, place=place:

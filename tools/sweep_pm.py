@@ -66,8 +66,6 @@ def main():
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="tile", flags=fl)))
     direct = [(f"pm_direct_{w}wpc", w << L.RTI_KERNEL_TILE_WAVES_SHIFT) for w in (4, 8, 12)]
     direct += [(f"pm_direct_gens{g}", g << L.RTI_KERNEL_CHUNKS_SHIFT) for g in (2, 4, 6)]
-    direct += [("pm_direct_contig", L.RTI_KERNEL_ROTATE), ("pm_direct_plain_loads", L.RTI_KERNEL_PINV_LDS),
-               ("pm_direct_contig_gens4", L.RTI_KERNEL_ROTATE | (4 << L.RTI_KERNEL_CHUNKS_SHIFT))]
     for name, fl in direct:
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
         if plan // 100000000 == L.RTI_PM_DIRECT:
