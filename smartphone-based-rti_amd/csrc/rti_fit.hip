@@ -1098,7 +1098,7 @@ int launch_tile_w_t(const FitArgs& a) {
 // wide-workgroup tile (fp32): rc 4 or 8, 8 waves, loads 1 or 2 steps ahead
 template <int RC, int AHEAD, int W = 8>
 int launch_tile_w_l(const FitArgs& a) {
-  if constexpr (RC == 16 && AHEAD == 0) {  // AUTO's kernel with non-temporal coefficient stores (measurement)
+  if constexpr (RC == 16 && AHEAD == 0) {  // AUTO's kernel: non-temporal coefficient stores
     if ((a.mode & VM_NTS) && a.nt)
       return a.layout == RTI_COEF_PLANAR ? launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, true, 2>(a)
                                          : launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PIXEL_MAJOR, true, 2>(a);
@@ -1374,8 +1374,9 @@ extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, in
     // PTM-6 pixel-major coefficients leave through LDS as whole 1 KiB rows per store
     // instruction: with wide lanes the direct 96-B-strided stores raised WRITE_SIZE to 1.46x
     // the coefficient bytes (c3 0.573 -> 0.549 ms, c2 0.082 -> 0.072 ms staged)
-    a.mode = VM_NT | (k == 6 ? VM_STAGE : 0) | ((kernel & RTI_KERNEL_ROTATE) ? VM_ROT : 0) |
-             ((k == 16 && (kernel & RTI_KERNEL_NT_STORE)) ? VM_NTS : 0);
+    // HSH-16 (tile_w<16,8,0>): non-temporal coefficient stores, the one store placement that beat the mixed
+    // read/write probe's (c4 3.39 against 3.57 ms, profiles/r04r_c4_nts_sweep.log)
+    a.mode = VM_NT | (k == 6 ? VM_STAGE : 0) | ((kernel & RTI_KERNEL_ROTATE) ? VM_ROT : 0) | (k == 16 ? VM_NTS : 0);
   }
   Generations gens;  // one launch unless AUTO splits it (launch generations, above)
   if (a.nc == 0) {

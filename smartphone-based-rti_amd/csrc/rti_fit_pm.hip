@@ -1082,12 +1082,13 @@ extern "C" int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int
   const int64_t cs = channel_stride ? channel_stride : P * ps;
   if (!pm_dma_shape(k, N, in_dtype, P, C, ps, cs) || (kernel & 0xff) == RTI_KERNEL_VALU) return 0;
   const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
-  if ((kernel & 0xff) == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE) && N % 4 == 0 && pm_direct_ns(N))
-    return RTI_PM_DIRECT * 100000000 + pm_direct_ns(N) * 1000 + (w_req ? w_req : PM_DIRECT_WPC);
-  if ((kernel & 0xff) == RTI_KERNEL_AUTO) {
+  const bool stage = (kernel & RTI_KERNEL_STAGE) != 0;
+  if ((kernel & 0xff) == RTI_KERNEL_AUTO && !stage) {
     const VPlan vp = vstream_plan(k, N, 4, w_req);
     if (vp.W && (int64_t)C * P * k * 4 < 0xFFFFFFF0ll) return RTI_PM_VALU_STREAM * 100000000 + (vp.ring >> 10) * 1000 + vp.W;
   }
+  if ((kernel & 0xff) == RTI_KERNEL_AUTO && N % 4 == 0 && pm_direct_ns(N))
+    return RTI_PM_DIRECT * 100000000 + pm_direct_ns(N) * 1000 + (w_req ? w_req : PM_DIRECT_WPC);
   if ((kernel & 0xff) != RTI_KERNEL_TILE) {
     const StreamPlan sp = stream_plan(N, 4, w_req, c_req);
     if (sp.W) return RTI_PM_MFMA_STREAM * 100000000 + (sp.ring >> 10) * 1000 + sp.W;
@@ -1131,19 +1132,22 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
                       rti_fit_shared_pm_plan(k, N, in_dtype, P, C, a.ps, a.cs, kernel) != 0 &&
                       aligned_to(I, 16) && aligned_to(coef, 16) && a.ocs % 4 == 0;
   const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
-  if (dma_ok && sel == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE) && N % 4 == 0 && pm_direct_ns(N)) {
-    DirectOpts o;  // straight to registers.  Measurement flags: TILE_WAVES(w) waves per CU, CHUNKS(n) launch
-    if (w_req) o.wpc = w_req;  // generations
-    if (c_req) o.gens = c_req;
-    const int st = in_dtype == RTI_F32 ? launch_direct<float>(a, o) : launch_direct<int32_t>(a, o);
-    return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
-  }
-  if (dma_ok && sel == RTI_KERNEL_AUTO) {  // k <= 9: one pixel per lane, packed FMAs
+  // AUTO: k <= 9 the VALU stream (one pixel per lane, packed FMAs: c3 0.645 ms against 0.682 direct), k = 16
+  // the direct form (c4 3.754 against 3.858 ms for the MFMA stream; profiles/r04r_pm_sweep_c*.log);
+  // RTI_KERNEL_STAGE with AUTO forces the direct form (its coefficients are staged through LDS)
+  if (dma_ok && sel == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE)) {
     const VPlan vp = vstream_plan(k, N, es, w_req);
     if (vp.W && vstream_coef_ok(a)) {
       const int st = in_dtype == RTI_F32 ? launch_vstream<float>(a, vp) : launch_vstream<int32_t>(a, vp);
       return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
     }
+  }
+  if (dma_ok && sel == RTI_KERNEL_AUTO && N % 4 == 0 && pm_direct_ns(N)) {
+    DirectOpts o;  // straight to registers.  Measurement flags: TILE_WAVES(w) waves per CU, CHUNKS(n) launch
+    if (w_req) o.wpc = w_req;  // generations
+    if (c_req) o.gens = c_req;
+    const int st = in_dtype == RTI_F32 ? launch_direct<float>(a, o) : launch_direct<int32_t>(a, o);
+    return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
   }
   if (dma_ok) {
     StreamPlan sp;

@@ -158,7 +158,8 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int TP16 = 128;  // pixels per workgroup tile (4 blocks of 32)
 constexpr int KSMAX = 8;   // k-steps (16 lights each) the pipelined sweep holds in registers: N <= 128
 
-template <typename T, typename TO, bool VEC>
+// NTS: non-temporal table stores (AUTO; false = plain stores, a measurement variant: RTI_OP_PLAIN_STORES=1)
+template <typename T, typename TO, bool VEC, bool NTS = true>
 __global__ void __launch_bounds__(256)
 apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int E, int N,
               const T* __restrict__ I, int64_t P, int64_t lstride, int64_t cstride, TO* __restrict__ out,
@@ -281,8 +282,12 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
       TO* __restrict__ rp = lb + (int64_t)dr * orow;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        if (!guard || (row < E && p0 + 32 * b + r < P))
-          __builtin_nontemporal_store(cvt_out<TO>(acc[b][reg] * oscale), rp + 32 * b);
+        if (!guard || (row < E && p0 + 32 * b + r < P)) {
+          if constexpr (NTS)
+            __builtin_nontemporal_store(cvt_out<TO>(acc[b][reg] * oscale), rp + 32 * b);
+          else
+            rp[32 * b] = cvt_out<TO>(acc[b][reg] * oscale);
+        }
       }
     }
   };
@@ -364,18 +369,15 @@ int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int 
   unsigned gy = (unsigned)std::max(1, std::min(nwb, (int)((want + gx - 1) / gx)));
   if (const char* e = getenv("RTI_OP_GY")) gy = (unsigned)std::max(1, std::min(nwb, atoi(e)));  // measurement
   dim3 grid(gx, gy, C);
-  if (lds > 65536) {
-    auto k = vec ? apply_op_f16s<T, TO, true> : apply_op_f16s<T, TO, false>;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-        hipSuccess)
-      return fail(RTI_ERR_HIP, "rti_apply_operator_f16: cannot reserve %zu B of LDS", lds);
-  }
-  if (vec)
-    hipLaunchKernelGGL((apply_op_f16s<T, TO, true>), grid, dim3(256), lds, s, hi, lo, Kp, inv_s, E, N,
-                       static_cast<const T*>(I), P, ls, cs, static_cast<TO*>(out), orow, ocs);
-  else
-    hipLaunchKernelGGL((apply_op_f16s<T, TO, false>), grid, dim3(256), lds, s, hi, lo, Kp, inv_s, E, N,
-                       static_cast<const T*>(I), P, ls, cs, static_cast<TO*>(out), orow, ocs);
+  const char* ps = getenv("RTI_OP_PLAIN_STORES");  // measurement
+  auto k = vec ? apply_op_f16s<T, TO, true> : apply_op_f16s<T, TO, false>;
+  if (vec && ps && atoi(ps)) k = apply_op_f16s<T, TO, true, false>;
+  if (lds > 65536 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return fail(RTI_ERR_HIP, "rti_apply_operator_f16: cannot reserve %zu B of LDS", lds);
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, hi, lo, Kp, inv_s, E, N, static_cast<const T*>(I), P, ls, cs,
+                     static_cast<TO*>(out), orow, ocs);
   return check_launch("rti_apply_operator_f16");
 }
 

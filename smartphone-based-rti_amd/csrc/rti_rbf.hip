@@ -903,7 +903,9 @@ rbf_solve_fp64(const float* __restrict__ lu, const float* __restrict__ lv, const
 // capture over ≈ 68 s.  For those N the same bordered system (see rbf_solve_gji:
 // S = −(HAH)[:n, :n] symmetric positive definite, n = N − 1) is factored S = L Lᵀ in fp64 — SciPy's fp64
 // accuracy without refinement — by a right-looking blocked Cholesky whose matrix lives in a per-workgroup
-// slot of global memory ([ld][ld] doubles, lower triangle, L2/MALL-resident while the slot is hot):
+// slot of global memory (the lower triangle in packed rows, 4·ld² bytes; r04: the packed slot and a
+// left-looking form that writes each L panel once were measured and neither moved the solve — c8n400 478 ms
+// full or packed, 1384–1584 ms left-looking, DESIGN §4.3 — the panel loop is latency-bound, not slot-bound):
 //   setup: A's row sums from every distance of a row (g = A u needs no column pass over a stored A), then
 //   S written in one pass from the distances evaluated again (write-only);
 //   per panel of NB columns: the panel rows [k0, n) are staged in LDS (a short last panel padded with the
@@ -924,13 +926,9 @@ constexpr int RBF_CH_THREADS = 512;
 constexpr size_t RBF_CH_LDS = 160 * 1024 - 256;  // dynamic LDS per workgroup (the static part is < 256 B)
 
 // LDS of one workgroup: the panel [N][NB + 1] doubles (a bank shift per row), the two right-hand sides /
-// solutions [2][N] doubles, the nodes [2][N] floats, and the left-looking form's staged block
-// [max(CH_QC, NB + 1)][NB] doubles.
-constexpr int CH_QC = 32;  // columns of L per left-looking update chunk
-__host__ __device__ constexpr size_t chol_lds_bytes(int N, int NB) {
-  return (size_t)N * (8 * NB + 8 + 16 + 8) + (size_t)8 * NB * (CH_QC > NB + 1 ? CH_QC : NB + 1);
-}
-// widest panel whose LDS fits: 32 to N = 538, 16 to 996, 8 to 1682, 4 to 2540, 2 to 3397, 1 to 4083
+// solutions [2][N] doubles and the nodes [2][N] floats
+__host__ __device__ constexpr size_t chol_lds_bytes(int N, int NB) { return (size_t)N * (8 * NB + 8 + 16 + 8); }
+// widest panel whose LDS fits: 32 to N = 568, 16 to 1022, 8 to 1704, 4 to 2556, 2 to 3408, 1 to 4089
 // (0: too many lights).  The narrow panels are slow (the trailing triangle is rewritten every NB columns:
 // ≈ 16·n³/(6·NB) bytes of slot traffic per pixel) but keep the reference's uncapped N = frames/8 − failures
 // (analysis.py:120,152) solvable to a 17-minute capture at 30 fps.
@@ -942,13 +940,17 @@ __host__ __device__ constexpr int chol_nb(int N) {
          : chol_lds_bytes(N, 2) <= RBF_CH_LDS ? 2
          : chol_lds_bytes(N, 1) <= RBF_CH_LDS ? 1 : 0;
 }
-constexpr int RBF_CH_MAX_N = 4083;
-static_assert(chol_nb(538) == 32 && chol_nb(539) == 16 && chol_nb(2540) == 4 && chol_nb(2541) == 2 &&
+constexpr int RBF_CH_MAX_N = 4089;
+static_assert(chol_nb(568) == 32 && chol_nb(569) == 16 && chol_nb(2556) == 4 && chol_nb(2557) == 2 &&
                   chol_nb(RBF_CH_MAX_N) == 1 && chol_nb(RBF_CH_MAX_N + 1) == 0, "RBF_CH_MAX_N");
 
 __host__ __device__ constexpr int chol_ld(int N) { return (N + 31) / 32 * 32; }
-// per-workgroup slot in global memory: M [ld][ld] (lower triangle) + the vectors g (= A u), c, m ([ld] each)
-__host__ __device__ constexpr int64_t chol_slot_doubles(int N) { return (int64_t)chol_ld(N) * chol_ld(N) + 3 * chol_ld(N); }
+// per-workgroup slot in global memory: the lower triangle of M in packed rows + the vectors g (= A u), c, m
+// ([ld] each)
+__host__ __device__ constexpr int64_t chol_matrix_doubles(int N) {
+  return ((int64_t)chol_ld(N) * (chol_ld(N) + 1) / 2 + 31) / 32 * 32;
+}
+__host__ __device__ constexpr int64_t chol_slot_doubles(int N) { return chol_matrix_doubles(N) + 3 * chol_ld(N); }
 
 // Phase timer for tools/probe/chol_probe.hip (compiled in only there): per workgroup, the steady-clock
 // ticks spent in each phase, summed over its pixels (a barrier closes every phase).
@@ -969,12 +971,7 @@ __device__ unsigned long long rti_chol_prof[1024][16];
   } while (0)
 #endif
 
-// LL (left-looking, r04): S is never stored — each panel is staged from the distances and updated from the
-// panels already factored, L[k0.., 0..k0)·L[k0..k0+kb, 0..k0)ᵀ, read from a COLUMN-major L (LT[q][i] = L[i][q],
-// coalesced over the panel rows); each L panel is written once; the backward substitution stages L's
-// column blocks through LDS.  Slot traffic per pixel ≈ 8·(n³/(6·NB) + n²) bytes against the right-looking
-// form's 16·n³/(6·NB) (n = 400, NB = 32: 3.9 MB against 7.3 MB; writes 0.64 MB against 2.7 MB).
-template <int NB, typename T, bool LL = false>
+template <int NB, typename T>
 __global__ void __launch_bounds__(RBF_CH_THREADS)
 rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
                double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status,
@@ -987,13 +984,14 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
   double* y2 = y1 + N;                                       // m  -> L⁻¹m  -> S⁻¹m
   float* xs = reinterpret_cast<float*>(y2 + N);
   float* ys = xs + N;
-  double* bq = reinterpret_cast<double*>(ys + N);  // LL: [CH_QC][NB] staged L block / the backward diagonal block
   __shared__ double red[TH / 64];
   __shared__ int s_bad;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n = N - 1, ld = chol_ld(N);
   double* M = ws + (int64_t)blockIdx.x * chol_slot_doubles(N);
-  double* gv = M + (int64_t)ld * ld;  // g = A u
+  // the lower triangle in packed rows (row i at i(i+1)/2): 4·ld² bytes per slot
+  auto at = [&](int i, int j) -> int64_t { return (int64_t)i * (i + 1) / 2 + j; };
+  double* gv = M + chol_matrix_doubles(N);  // g = A u
   double* cv = gv + ld;               // c = H b
   double* mv = cv + ld;               // m = (HAH)[:n, n], μ at n
   const double e = 1.0 / sqrt((double)N), beta = 1.0 / (1.0 - e);  // H = I − β u uᵀ, u = e·1 − e_n
@@ -1080,11 +1078,9 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       const double ci = y1[i] - beta * u(i) * utb, mi = hah(n, i, i < n ? dist(n, i) : 0.0);
       cv[i] = ci, mv[i] = mi, y1[i] = ci, y2[i] = mi;
     }
-    // S = −(HAH)[:n, :n] into M, lower triangle, one wave per row (the distances again: a write-only pass);
-    // the left-looking form computes S's panels where it stages them instead
-    if constexpr (!LL)
-      for (int i = wave; i < n; i += TH / 64)
-        for (int j = lane; j <= i; j += 64) M[(int64_t)i * ld + j] = -hah(i, j, dist(i, j));
+    // S = −(HAH)[:n, :n] into M, lower triangle, one wave per row (the distances again: a write-only pass)
+    for (int i = wave; i < n; i += TH / 64)
+      for (int j = lane; j <= i; j += 64) M[at(i, j)] = -hah(i, j, dist(i, j));
     __syncthreads();
     CH_MARK(3);
 
@@ -1096,91 +1092,10 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       for (int idx = t; idx < max(rows, NB) * NB; idx += TH) {
         const int r = idx / NB, c = idx - r * NB;
         double v = r == c && r >= kb ? 1.0 : 0.0;
-        if (c < kb && c <= r && r < rows) {
-          if constexpr (LL)
-            v = -hah(k0 + r, k0 + c, dist(k0 + r, k0 + c));
-          else
-            v = M[(int64_t)(k0 + r) * ld + k0 + c];
-        }
+        if (c < kb && c <= r && r < rows) v = M[at(k0 + r, k0 + c)];
         pan[r * LDP + c] = v;
       }
       __syncthreads();
-      if constexpr (LL) {
-        // left-looking update: pan[r][c] −= Σ_{q < k0} L[k0+r][q]·L[k0+c][q], in chunks of CH_QC columns q;
-        // L[k0+c][q] (c < kb) staged in LDS, L[k0+r][q] = LT[q][k0+r] read coalesced by thread r
-        if (rows <= TH) {
-          // one row per thread, chunks of QP columns q: the next chunk's L values and its staged L[k0+c][q]
-          // element are loaded into registers while the current chunk's FMAs run; the sums stay in registers
-          // across the chunks (one LDS update at the end)
-          constexpr int QP = NB >= 32 ? 8 : 16;  // (<= CH_QC rows of bq)
-          const int r = t;
-          const bool act = r < rows;
-          const int nch = (k0 + QP - 1) / QP;
-          const double* lrow = M + k0 + r;  // L[k0+r][q] = LT[q][k0+r]
-          const int bqq = t / NB, bc = t - (t / NB) * NB;  // this thread's staged element (t < QP·NB)
-          const bool bok = t < QP * NB && bc < kb;
-          double acc[NB], li[QP];
-#pragma unroll
-          for (int c = 0; c < NB; ++c) acc[c] = 0.0;
-#pragma unroll
-          for (int u = 0; u < QP; ++u) li[u] = (act && u < k0) ? lrow[(int64_t)u * ld] : 0.0;
-          double bn = (bok && bqq < k0) ? M[(int64_t)bqq * ld + k0 + bc] : 0.0;
-          for (int ch = 0; ch < nch; ++ch) {
-            if (t < QP * NB) bq[t] = bn;  // (zeros past the chunk: 0·stale could be NaN)
-            __syncthreads();
-            double cur[QP];
-#pragma unroll
-            for (int u = 0; u < QP; ++u) cur[u] = li[u];
-            const int nq = (ch + 1) * QP;
-#pragma unroll
-            for (int u = 0; u < QP; ++u) li[u] = (act && nq + u < k0) ? lrow[(int64_t)(nq + u) * ld] : 0.0;
-            bn = (bok && nq + bqq < k0) ? M[(int64_t)(nq + bqq) * ld + k0 + bc] : 0.0;
-#pragma unroll
-            for (int u = 0; u < QP; ++u)
-#pragma unroll
-              for (int c = 0; c < NB; ++c) acc[c] = fma(cur[u], bq[u * NB + c], acc[c]);
-            __syncthreads();  // bq is restaged
-          }
-          if (act)
-#pragma unroll
-            for (int c = 0; c < NB; ++c)
-              if (c < kb && (r >= kb || c <= r)) pan[r * LDP + c] -= acc[c];
-          __syncthreads();
-        } else
-        for (int qb = 0; qb < k0; qb += CH_QC) {
-          const int qc = min(CH_QC, k0 - qb);
-          for (int idx = t; idx < qc * NB; idx += TH) {
-            const int q = idx / NB, c = idx - q * NB;
-            bq[idx] = c < kb ? M[(int64_t)(qb + q) * ld + k0 + c] : 0.0;
-          }
-          __syncthreads();
-          for (int r = t; r < rows; r += TH) {
-            double acc[NB];
-#pragma unroll
-            for (int c = 0; c < NB; ++c) acc[c] = 0.0;
-            const double* lcol = M + (int64_t)qb * ld + k0 + r;
-            int q = 0;
-            for (; q + 4 <= qc; q += 4) {
-              double li[4];
-#pragma unroll
-              for (int u = 0; u < 4; ++u) li[u] = lcol[(int64_t)(q + u) * ld];
-#pragma unroll
-              for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int c = 0; c < NB; ++c) acc[c] = fma(li[u], bq[(q + u) * NB + c], acc[c]);
-            }
-            for (; q < qc; ++q) {
-              const double li = lcol[(int64_t)q * ld];
-#pragma unroll
-              for (int c = 0; c < NB; ++c) acc[c] = fma(li, bq[q * NB + c], acc[c]);
-            }
-#pragma unroll
-            for (int c = 0; c < NB; ++c)
-              if (c < kb && (r >= kb || c <= r)) pan[r * LDP + c] -= acc[c];
-          }
-          __syncthreads();  // bq is restaged
-        }
-      }
       CH_MARK(4);
       if (wave == 0 && lane < NB) {  // the diagonal block in place in LDS, lane r updating row r (right-looking):
         // the pivot and column c of L are uniform-address (broadcast) reads, the pivot's inverse square root is
@@ -1233,16 +1148,9 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       }
       __syncthreads();
       CH_MARK(6);
-      if constexpr (LL) {  // write L's panel once, column-major: LT[k0+c][k0+r], coalesced over r
-        for (int idx = t; idx < rows * kb; idx += TH) {
-          const int c = idx / rows, r = idx - c * rows;
-          if (c <= r) M[(int64_t)(k0 + c) * ld + k0 + r] = pan[r * LDP + c];
-        }
-      } else {
-        for (int idx = t; idx < rows * NB; idx += TH) {  // write L's panel back (for the backward substitution)
-          const int r = idx / NB, c = idx - r * NB;
-          if (c < kb && c <= r) M[(int64_t)(k0 + r) * ld + k0 + c] = pan[r * LDP + c];
-        }
+      for (int idx = t; idx < rows * NB; idx += TH) {  // write L's panel back (for the backward substitution)
+        const int r = idx / NB, c = idx - r * NB;
+        if (c < kb && c <= r) M[at(k0 + r, k0 + c)] = pan[r * LDP + c];
       }
       for (int r = kb + t; r < rows; r += TH) {  // y[i] −= L[i][k0:k0+kb]·y_block (LDS)
         double s1 = y1[k0 + r], s2 = y2[k0 + r];
@@ -1259,7 +1167,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       // (x, y) = (lane & 7, lane >> 3) owns rows y + 8a (a < 8) and columns x + 8b (b < 4) — each LDS read
       // touches 8 distinct panel rows (distinct banks with the NB + 1 pitch), broadcast over 8 lanes;
       // 12 reads per 32 fp64 FMAs
-      const int m = rows - kb, T64 = (m + 63) / 64, nst = LL ? 0 : T64 * (T64 + 1);  // row tile I: 2I + 2 col tiles
+      const int m = rows - kb, T64 = (m + 63) / 64, nst = T64 * (T64 + 1);  // row tile I: 2I + 2 col tiles
       const int lx = lane & 7, ly = lane >> 3;
       for (int st = wave; st < nst; st += TH / 64) {
         int I64 = 0;
@@ -1272,7 +1180,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
 #pragma unroll
         for (int a = 0; a < 8; ++a) {
           const int rr = min(ri + 8 * a, rows - 1);
-          const double* row = M + (int64_t)(k0 + rr) * ld + k0;
+          const double* row = M + at(k0 + rr, k0);
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
             acc[a][b] = 0.0;
@@ -1293,7 +1201,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
 #pragma unroll
         for (int a = 0; a < 8; ++a) {
           if (ri + 8 * a >= rows) continue;
-          double* row = M + (int64_t)(k0 + ri + 8 * a) * ld + k0;
+          double* row = M + at(k0 + ri + 8 * a, k0);
 #pragma unroll
           for (int b = 0; b < 4; ++b)
             if (rj + 8 * b < rows && rj + 8 * b <= ri + 8 * a) row[rj + 8 * b] = old[a][b] - acc[a][b];
@@ -1312,44 +1220,14 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
     // ---- Lᵀ z = y (backward), blocked by NB: diagonal blocks staged in LDS (the panel is free) --------
     // Each thread's first row of the off-diagonal update (i = t) is loaded with the diagonal block, so one
     // global-memory latency per block sits on the serial path.
-    if constexpr (LL) {
-      // column-major L: the diagonal block (LT[k0+c][k0+r]) goes to bq, the block's columns of the rows above
-      // (L[k0+q][i] = LT[i][k0+q], i < k0: kb contiguous doubles per row) to the panel, both staged coalesced
-      for (int k0 = (n - 1) / NB * NB; k0 >= 0; k0 -= NB) {
-        const int kb = min(NB, n - k0);
-        for (int idx = t; idx < NB * NB; idx += TH) {  // (a short block padded with the identity)
-          const int r = idx / NB, c = idx - r * NB;
-          const double l = r < kb && c <= r ? M[(int64_t)(k0 + c) * ld + k0 + r] : (r == c ? 1.0 : 0.0);
-          bq[r * LDP + c] = l;
-          if (c == r) bq[r * LDP + NB] = 1.0 / l;
-        }
-        for (int idx = t; idx < k0 * kb; idx += TH) {
-          const int i = idx / kb, q = idx - i * kb;
-          pan[i * LDP + q] = M[(int64_t)i * ld + k0 + q];
-        }
-        __syncthreads();
-        if (wave == 0) diag_bwd(bq, kb, y1 + k0, y2 + k0);
-        __syncthreads();
-        for (int i = t; i < k0; i += TH) {  // y[i] −= Σ_q L[k0+q][i]·z[k0+q]
-          double s1 = y1[i], s2 = y2[i];
-          for (int q = 0; q < kb; ++q) {
-            const double l = pan[i * LDP + q];
-            s1 = fma(-l, y1[k0 + q], s1);
-            s2 = fma(-l, y2[k0 + q], s2);
-          }
-          y1[i] = s1, y2[i] = s2;
-        }
-        __syncthreads();
-      }
-    } else
     for (int k0 = (n - 1) / NB * NB; k0 >= 0; k0 -= NB) {
       const int kb = min(NB, n - k0);
       double lp[NB];
 #pragma unroll
-      for (int q = 0; q < NB; ++q) lp[q] = t < k0 ? M[(int64_t)(k0 + min(q, kb - 1)) * ld + t] : 0.0;
+      for (int q = 0; q < NB; ++q) lp[q] = t < k0 ? M[at(k0 + min(q, kb - 1), t)] : 0.0;
       for (int idx = t; idx < NB * NB; idx += TH) {  // (a short block padded with the identity)
         const int r = idx / NB, c = idx - r * NB;
-        const double l = r < kb && c <= r ? M[(int64_t)(k0 + r) * ld + k0 + c] : (r == c ? 1.0 : 0.0);
+        const double l = r < kb && c <= r ? M[at(k0 + r, k0 + c)] : (r == c ? 1.0 : 0.0);
         pan[r * LDP + c] = l;
         if (c == r) pan[r * LDP + NB] = 1.0 / l;
       }
@@ -1368,7 +1246,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         y1[i] = s1, y2[i] = s2;
       };
       if (t < k0) upd(t, [&](int q) { return lp[q]; });
-      for (int i = t + TH; i < k0; i += TH) upd(i, [&](int q) { return M[(int64_t)(k0 + min(q, kb - 1)) * ld + i]; });
+      for (int i = t + TH; i < k0; i += TH) upd(i, [&](int q) { return M[at(k0 + min(q, kb - 1), i)]; });
       __syncthreads();
     }
     CH_MARK(9);
@@ -1408,11 +1286,6 @@ int gji_min_n() {
   static const int v = env_int("RTI_RBF_GJI_MIN_N", RBF_GJ_MAX_N + 1);
   return v;
 }
-// RTI_RBF_CHOL_LL: 1 = the left-looking Cholesky (rbf_solve_chol<.., true>), 0 = right-looking (A/B)
-bool chol_left_looking() {
-  static const int v = env_int("RTI_RBF_CHOL_LL", 1);
-  return v != 0;
-}
 int gji_refine() {
   static const int v = env_int("RTI_RBF_GJI_REFINE", RBF_GJI_MAX_REFINE);
   return v;
@@ -1435,17 +1308,6 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
                                 (int)lds);
       hipLaunchKernelGGL(kern, dim3(cg), dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
     };
-    if (chol_left_looking()) {
-      switch (chol_nb(N)) {
-        case 32: go(rbf_solve_chol<32, T, true>); break;
-        case 16: go(rbf_solve_chol<16, T, true>); break;
-        case 8: go(rbf_solve_chol<8, T, true>); break;
-        case 4: go(rbf_solve_chol<4, T, true>); break;
-        case 2: go(rbf_solve_chol<2, T, true>); break;
-        default: go(rbf_solve_chol<1, T, true>); break;
-      }
-      return;
-    }
     switch (chol_nb(N)) {
       case 32: go(rbf_solve_chol<32, T>); break;
       case 16: go(rbf_solve_chol<16, T>); break;

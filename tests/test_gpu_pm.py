@@ -20,9 +20,11 @@ def test_golden_256x256_N20_pixel_major(cuda):
     d = golden("ptm_shared_256x256_N20.npz")
     Ipm = torch.as_tensor(np.ascontiguousarray(np.moveaxis(d["I"], 0, -1))).to(cuda, torch.float32)  # [256, 256, 20]
     plan = L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, 0)
-    assert plan // 10**8 == L.RTI_PM_DIRECT, plan  # AUTO (N % 4 == 0): straight to registers
+    assert plan // 10**8 == L.RTI_PM_VALU_STREAM, plan  # AUTO for PTM-6: the packed-FMA stream
     plan = L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, L.RTI_KERNEL_STAGE)
-    assert plan // 10**8 == L.RTI_PM_VALU_STREAM, plan  # AUTO through the LDS ring: the packed-FMA stream
+    assert plan // 10**8 == L.RTI_PM_DIRECT, plan  # AUTO | STAGE: straight to registers (AUTO for HSH-16)
+    plan = L.lib().rti_fit_shared_pm_plan(16, 20, L.RTI_F32, 256 * 256, 1, 0, 0, 0)
+    assert plan // 10**8 == L.RTI_PM_DIRECT, plan
     for layout in ("pixel", "planar"):
         coef = rti.fit(Ipm, d["lu"], d["lv"], stack="pixel", layout=layout).cpu().numpy()
         if layout == "planar":
@@ -73,14 +75,15 @@ def test_pm_shapes_vs_fp64(cuda, basis, N, in_dtype):
         ref = _ref(I, pinv64)
         Id = torch.as_tensor(I, device=cuda).to(in_dtype)
         for layout in ("pixel", "planar"):
-            coef = torch.full((2, P, k) if layout == "pixel" else (2, k, P), float("nan"), device=cuda)
-            rti.api.fit_shared_pm_into(pv, Id, coef, k=k, layout=layout)
-            got = coef.cpu().numpy()
-            if layout == "planar":
-                got = np.moveaxis(got, 1, 2)
-            for c in range(2):
-                err, ok = coef_close(got[c], ref[c])
-                assert ok, (P, layout, c, err)
+            for flags in (0, L.RTI_KERNEL_STAGE):  # AUTO, and the direct form for every k
+                coef = torch.full((2, P, k) if layout == "pixel" else (2, k, P), float("nan"), device=cuda)
+                rti.api.fit_shared_pm_into(pv, Id, coef, k=k, layout=layout, flags=flags)
+                got = coef.cpu().numpy()
+                if layout == "planar":
+                    got = np.moveaxis(got, 1, 2)
+                for c in range(2):
+                    err, ok = coef_close(got[c], ref[c])
+                    assert ok, (P, layout, flags, c, err)
 
 
 @pytest.mark.parametrize("kern,g,w", [("tile", 1, 1), ("tile", 1, 4), ("tile", 2, 2), ("tile", 2, 5), ("tile", 4, 1),
@@ -88,7 +91,8 @@ def test_pm_shapes_vs_fp64(cuda, basis, N, in_dtype):
                                       ("mfma", 0, 6), ("mfma", 0, 8), ("mfma_contig", 0, 8), ("mfma_contig", 0, 3),
                                       ("mfma", 2, 8), ("mfma", 3, 4), ("mfma_contig", 2, 6),
                                       ("auto", 0, 4), ("auto", 0, 3), ("auto", 0, 2), ("auto", 0, 1),
-                                      ("auto", 0, 12), ("auto", 0, 8), ("auto_stage", 0, 4), ("auto_stage", 0, 2)])
+                                      ("auto_stage", 0, 12), ("auto_stage", 0, 8), ("auto_stage", 0, 4),
+                                      ("auto_stage", 2, 4)])
 @pytest.mark.parametrize("N", [20, 100, 33, 200])
 def test_pm_block_plans(cuda, kern, g, w, N):
     """kernel="tile" (the double-buffered block form): RTI_KERNEL_CHUNKS(G) / TILE_WAVES(W) = 16, 32 and
@@ -103,7 +107,7 @@ def test_pm_block_plans(cuda, kern, g, w, N):
     flags = (g << L.RTI_KERNEL_CHUNKS_SHIFT) | (w << L.RTI_KERNEL_TILE_WAVES_SHIFT)
     if kern == "mfma_contig":  # each wave one contiguous run of units instead of interleaved units
         kern, flags = "mfma", flags | L.RTI_KERNEL_ROTATE
-    if kern == "auto_stage":  # AUTO through the LDS ring (the VALU stream); plain AUTO: direct, W waves per CU
+    if kern == "auto_stage":  # the direct form: W waves per CU, CHUNKS(g) launch generations
         kern, flags = "auto", flags | L.RTI_KERNEL_STAGE
     if not L.lib().rti_fit_shared_pm_plan(k, N, L.RTI_F32, P, 3, 0, 0, flags | rti.api._KERNELS[kern]):
         pytest.skip("plan does not fit the LDS")
@@ -146,7 +150,8 @@ def test_pm_lane_fallback(cuda):
                                    kernel="mfma")
 
 
-@pytest.mark.parametrize("N,flags", [(21, 0), (20, 0), (20, L.RTI_KERNEL_STAGE), (100, 0), (104, 0)])
+@pytest.mark.parametrize("N,flags", [(21, 0), (20, 0), (20, L.RTI_KERNEL_STAGE), (100, L.RTI_KERNEL_STAGE),
+                                     (104, L.RTI_KERNEL_STAGE)])
 def test_pm_nan_stays_in_its_pixel(cuda, N, flags):
     """A NaN intensity makes its own pixel's coefficients NaN (0·NaN in the reference's matmul) and no
     other pixel's: the masked tail chunk (LDS forms) and the out-of-range lights of the last 16-light step

@@ -33,9 +33,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
     variants = args.gy.split(",")
 
-    def run(v):
-        if v == "auto":
+    def run(v):  # "auto", a grid.y, or "plain" (AUTO grid, plain instead of non-temporal table stores)
+        os.environ.pop("RTI_OP_PLAIN_STORES", None)
+        if v in ("auto", "plain"):
             os.environ.pop("RTI_OP_GY", None)
+            if v == "plain":
+                os.environ["RTI_OP_PLAIN_STORES"] = "1"
         else:
             os.environ["RTI_OP_GY"] = v
         wl.step(0)
