@@ -146,23 +146,28 @@ int rti_fit_shared(const float* pinv, int k, int N,
  *   coef[c][p][i] = Σ_n pinv[i][n] · I[c*channel_stride + p*pixel_stride + n]
  * (pixel_stride 0 = N, channel_stride 0 = P*pixel_stride).  pinv, coef, coef_layout and
  * coef_channel_stride as rti_fit_shared; in_dtype F32 / I32 / U8.
- * AUTO streams runs of 16-pixel groups (contiguous 16·N values each) HBM -> a per-wave LDS ring by 1-KiB
- * LDS-DMAs and contracts them there: one pixel per lane with packed FMAs for k <= 9, v_mfma_f32_16x16x4_f32
- * for k = 16 (RTI_KERNEL_MFMA: the MFMA stream for every k; RTI_KERNEL_TILE: a double-buffered block form).
+ * AUTO for k <= 9 streams runs of 16-pixel groups (contiguous 16·N values each) HBM -> a per-wave LDS ring by
+ * 1-KiB LDS-DMAs and contracts them there, one pixel per lane with packed FMAs; for k = 16 (and with
+ * RTI_KERNEL_STAGE for any k) the DIRECT form loads the groups straight into VGPRs as v_mfma_f32_16x16x4_f32
+ * operands and writes the coefficients in LDS-staged bursts (N % 4 == 0, N <= 256).  RTI_KERNEL_MFMA: the
+ * MFMA stream through the LDS ring for every k; RTI_KERNEL_TILE: a double-buffered block form.
  * These take F32 / I32 stacks, k in {6, 9, 16}, pixel_stride = N, P·N and channel_stride multiples of 4,
  * I and coef 16-byte aligned, P·k·4 < 2^31 and N within the LDS budget (rti_fit_shared_pm_plan);
  * RTI_KERNEL_MFMA / TILE fail with RTI_ERR_UNSUPPORTED outside that, AUTO and RTI_KERNEL_VALU run one lane
  * per pixel instead (any shape, uint8 included).  Measurement flags: RTI_KERNEL_TILE_WAVES(W) waves per
- * workgroup, RTI_KERNEL_CHUNKS(n) (MFMA stream: n× the smallest unit; block form: 16n-pixel blocks),
- * RTI_KERNEL_ROTATE (MFMA stream: each wave one contiguous run of units). */
+ * workgroup (direct form: per CU), RTI_KERNEL_CHUNKS(n) (MFMA stream: n× the smallest unit; block form:
+ * 16n-pixel blocks; direct form: n launch generations), RTI_KERNEL_ROTATE (MFMA stream: each wave one
+ * contiguous run of units), RTI_KERNEL_PINV_LDS (VALU stream: the weights by scalar loads instead of its
+ * LDS copy), RTI_KERNEL_ONE_LAUNCH / RTI_KERNEL_ROUNDS (VALU stream without stores / without arithmetic). */
 int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
                       int64_t pixel_stride, int64_t channel_stride,
                       float* coef, int coef_layout, int64_t coef_channel_stride,
                       int kernel, rti_stream_t stream);
 /* 0 if rti_fit_shared_pm runs one lane per pixel (the fallback) for this shape and kernel selection, else
  * form·10^8 + size·1000 + W: form RTI_PM_VALU_STREAM (AUTO, k <= 9: one pixel per lane, packed FMAs) or
- * RTI_PM_MFMA_STREAM (AUTO k = 16, RTI_KERNEL_MFMA) with size = KiB of LDS ring per wave, or RTI_PM_BLOCK
- * (RTI_KERNEL_TILE, or N too small for a ring) with size = pixels per block; W = waves per workgroup. */
+ * RTI_PM_MFMA_STREAM (RTI_KERNEL_MFMA) with size = KiB of LDS ring per wave and W = waves per workgroup,
+ * RTI_PM_BLOCK (RTI_KERNEL_TILE, or N too small for a ring) with size = pixels per block, or RTI_PM_DIRECT
+ * (AUTO k = 16, AUTO | RTI_KERNEL_STAGE) with size = 16-light steps and W = waves per CU. */
 #define RTI_PM_VALU_STREAM 1
 #define RTI_PM_MFMA_STREAM 2
 #define RTI_PM_BLOCK       3

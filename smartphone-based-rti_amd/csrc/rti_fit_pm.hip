@@ -412,7 +412,10 @@ fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
 // over the WHOLE coefficient array (per-lane 32-bit offsets; lanes past P or past the stream get an
 // out-of-range offset), so every block issues the same SB stores.
 // MODE (measurement, rti_fit_shared_pm flags): 0 = the fit; 1 = no coefficient stores (RTI_KERNEL_ONE_LAUNCH);
-// 2 = no arithmetic, the stream waited for and zeros stored (RTI_KERNEL_ROUNDS)
+// 2 = no arithmetic, the stream waited for and zeros stored (RTI_KERNEL_ROUNDS); 3 = the weights of the 4-light
+// steps by wave-uniform scalar loads into SGPRs (RTI_KERNEL_PINV_LDS's opposite, a measurement variant) instead
+// of broadcast ds_read_b128 from the LDS copy: 0.667 against 0.633 ms on c3 (profiles/r04s_pm_sweep_c3.log) —
+// the scalar loads return out of order, so each half step waits on lgkmcnt(0)
 template <int K, typename T, int LAYOUT, int ALIGN, int MODE = 0>
 __global__ void __launch_bounds__(256)
 fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
@@ -522,21 +525,37 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
       };
       const int n4 = N & ~3;
       if (n4 > 0) {
-        floatx4 x = rdx(0), w[K];
+        // weights pinv[i][n .. n+3]: broadcast reads of the LDS copy, or scalar loads into SGPRs (MODE 3)
+        auto wts = [&](int nn, int i) {
+          return MODE == 3 ? *reinterpret_cast<const floatx4*>(pinv + i * N + nn)
+                           : *reinterpret_cast<const floatx4*>(lw + nn * K + 4 * i);
+        };
+        // ping-pong register sets (no loop-carried copies): each half issues the next step's loads, then the
+        // FMAs of the step loaded one half earlier (scalar loads return out of order, so the only wait, at the
+        // top of a half, is lgkmcnt(0) on the loads issued a whole FMA block before)
+        floatx4 xa = rdx(0), xb, wa[K], wb[K];
 #pragma unroll
-        for (int i = 0; i < K; ++i) w[i] = *reinterpret_cast<const floatx4*>(lw + 4 * i);
-        for (n = 4; n < n4; n += 4) {
-          const floatx4 xn = rdx(n);
-          floatx4 wn[K];
+        for (int i = 0; i < K; ++i) wa[i] = wts(0, i);
+        for (n = 0; n < n4; n += 8) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this half's operands, before the next loads go out
+          if (n + 4 < n4) {
+            xb = rdx(n + 4);
 #pragma unroll
-          for (int i = 0; i < K; ++i) wn[i] = *reinterpret_cast<const floatx4*>(lw + n * K + 4 * i);
+            for (int i = 0; i < K; ++i) wb[i] = wts(n + 4, i);
+          }
           __builtin_amdgcn_sched_barrier(0);
-          step(x, w);
-          x = xn;
+          step(xa, wa);
+          if (n + 4 >= n4) break;
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          if (n + 8 < n4) {
+            xa = rdx(n + 8);
 #pragma unroll
-          for (int i = 0; i < K; ++i) w[i] = wn[i];
+            for (int i = 0; i < K; ++i) wa[i] = wts(n + 8, i);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          step(xb, wb);
         }
-        step(x, w);
+        n = n4;
       }
     }
     for (; n < N; ++n) {  // N % 4 (or every light when the rows are not 16-byte aligned)
@@ -946,8 +965,10 @@ VPlan vstream_plan(int k, int N, size_t es, int w_req) {
 
 template <int K, typename T, int LAYOUT, int ALIGN>
 int launch_vstream_t(const PmArgs& a, const VPlan& pl) {
-  auto kern = a.mode == 1 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 1>
-                          : (a.mode == 2 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 2> : fit_pm_vstream<K, T, LAYOUT, ALIGN, 0>);
+  auto kern = a.mode == 1   ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 1>
+              : a.mode == 2 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 2>
+              : a.mode == 3 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 3>
+                            : fit_pm_vstream<K, T, LAYOUT, ALIGN, 0>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)pl.lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
@@ -1121,7 +1142,7 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
   a.layout = coef_layout;
   a.ocs = coef_channel_stride ? coef_channel_stride : P * k;
   a.stream = (hipStream_t)stream;
-  a.mode = (kernel & RTI_KERNEL_ONE_LAUNCH) ? 1 : ((kernel & RTI_KERNEL_ROUNDS) ? 2 : 0);
+  a.mode = (kernel & RTI_KERNEL_ONE_LAUNCH) ? 1 : (kernel & RTI_KERNEL_ROUNDS) ? 2 : (kernel & RTI_KERNEL_PINV_LDS) ? 3 : 0;
   if (a.ps < N) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: pixel_stride < N");
   if (C > 1 && a.cs < P * a.ps) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: channel_stride");
   if (C > 1 && a.ocs < P * k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: coef_channel_stride");

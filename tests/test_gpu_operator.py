@@ -193,7 +193,7 @@ def test_compat_default_interpolation_perpixel(cuda):
 
 
 @pytest.mark.parametrize("n", [2, 6, 37, 64, 65, 80, 81, 100, 127, 128, 129, 160, 200, 248, 249, 255, 256,
-                               257, 300, 400, 512, 568, 569, 1100, 1800, 2557, 3000])
+                               257, 300, 400, 512, 568, 569, 1100, 1800, 2557, 3000, 3500])
 def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     """Every solver of rti_rbf_perpixel: fp64 register Gauss-Jordan (N <= 80) and the register-blocked
     fp32 Gauss-Jordan inverse + fp64 refinement on the full 16x16 block grid (N <= 128), the
@@ -201,7 +201,8 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     reference at N = 200), and above 256 lights the blocked fp64 Cholesky (panels of 32 lights to N = 568,
     16 to 1022, 8 to 1704, 4 to 2556, 2 to 3408, 1 to 4089; the reference takes N = frames/8 with no cap,
     analysis.py:120,152), each with the reference's per-pixel geometry, against SciPy's fp64 solve restated
-    in the oracle.  (The two largest N run on 4 pixels: each pixel is one workgroup's seconds of work.)"""
+    in the oracle.  (N > 1800 runs on 4 pixels: each pixel is one workgroup's seconds of work; 3500 takes the
+    one-column panel.)"""
     ys, xs = np.mgrid[0:3, 0:5] if n <= 1800 else np.mgrid[0:2, 0:2]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
@@ -278,7 +279,7 @@ def test_rbf_perpixel_fallback_many_pixels(cuda, n):
     assert (257 if n == 100 else 1) <= stats["fallback_px"] <= P
     for p in list(range(0, P, 37)) + [P - 1]:
         ref = o.rbf_linear(lu[p], lv[p], inten[p], qu, qv)
-        err, ok = relight_close(out[p], ref, rtol=1e-7)
+        err, ok = relight_close(out[p], ref, rtol=1e-6)  # cond(A) ~ 1e9..1e10: both fp64 solves err ~ cond·eps
         assert ok, (p, err)
 
 

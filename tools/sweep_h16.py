@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""The 8-bit shared fit (rti_fit_shared_h16) variants interleaved in ONE process, HIP events per launch, median
+of --rounds: load pipeline depth (RTI_KERNEL_TILE_DEPTH 2 / 3) and tiles per workgroup (RTI_KERNEL_CHUNKS),
+each checked bit-identical to the AUTO launch.
+
+  python tools/sweep_h16.py --config c3|c4 [--rounds 20] [--tpw 0,8,16]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "smartphone-based-rti_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import rti  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
+    ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--tpw", default="0")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    L = rti._lib
+    _, H, W, N, C, basis, _ = bench.CONFIGS[args.config]
+    k = rti.basis_terms(basis)
+    P = H * W
+    lu, lv = bench.synth_dirs(N, 2)
+    I8 = bench.synth_stack(H, W, N, C, basis, lu, lv, 1000, dev).clamp(0, 255).to(torch.uint8)
+    op = torch.as_tensor(rti.api.h16_operator(rti.pinv(lu, lv, basis)), device=dev)
+    coef = torch.empty((C, P, k), device=dev)
+    ref = torch.empty((C, P, k), device=dev)
+    variants = []
+    for tpw in [int(x) for x in args.tpw.split(",")]:
+        for depth in (2, 3):
+            fl = (tpw << L.RTI_KERNEL_CHUNKS_SHIFT) | (depth << L.RTI_KERNEL_TILE_DEPTH_SHIFT)
+            variants.append((f"h16_depth{depth}_tpw{tpw or 'auto'}",
+                             lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
+    rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
+    same = {}
+    for name, fn in variants:
+        coef.fill_(float("nan"))
+        fn()
+        torch.cuda.synchronize()
+        same[name] = bool(torch.equal(coef, ref))
+    stream = torch.cuda.current_stream(dev)
+    times = {name: [] for name, _ in variants}
+    for _ in range(args.rounds):
+        for name, fn in variants:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fn()
+            b.record(stream)
+            times[name].append((a, b))
+        torch.cuda.synchronize()
+    alg = 1.0 * P * N * C + 4.0 * P * k * C
+    res = {}
+    for name, _ in variants:
+        ms = float(np.median([a.elapsed_time(b) for a, b in times[name]]))
+        gbs = alg / (ms * 1e-3) / 1e9
+        res[name] = {"median_ms": ms, "GBps": gbs, "frac_8TBps": gbs / 8000.0, "bit_identical": same[name]}
+        print(f"{name:24s} {ms:.4f} ms  {gbs:.0f} GB/s ({gbs / 8000:.3f} of 8 TB/s)  same {same[name]}", flush=True)
+    print(json.dumps({"config": args.config, "alg_bytes": alg, "results": res}))
+
+
+if __name__ == "__main__":
+    main()

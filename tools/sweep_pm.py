@@ -77,6 +77,9 @@ def main():
             variants.append((f"pm_valu_w{w}_ring{plan % 100000000 // 1000}K",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
     variants.append(("pm_auto", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto")))
+    if k <= 9:  # the VALU stream's weights by scalar loads (SGPRs) instead of the LDS copy
+        variants.append(("pm_valu_sgpr_weights", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
+                                                                                 flags=L.RTI_KERNEL_PINV_LDS)))
     if k <= 9:  # measurement variants of the VALU stream: no stores / no arithmetic
         st = L.RTI_KERNEL_STAGE
         variants.append(("pm_valu_nostores", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
