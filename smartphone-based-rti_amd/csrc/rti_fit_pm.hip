@@ -630,7 +630,8 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
 template <int K, int NS>
 constexpr int pm_direct_run() { return K > 9 ? 12 : 24; }  // groups per run (a multiple of the depth)
 
-template <int K, typename T, int LAYOUT, int NS, int D>
+// NTS: the bursts' stores non-temporal (RTI_KERNEL_NT_STORE; pixel-major)
+template <int K, typename T, int LAYOUT, int NS, int D, bool NTS = false>
 __global__ void __launch_bounds__(256)
 fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
               float* __restrict__ coef, int64_t ocstride, int ngrp, int nrun, int r0, int tr) {
@@ -725,7 +726,7 @@ fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
         const floatx4 v = b < BYTES ? *reinterpret_cast<const floatx4*>(reinterpret_cast<const char*>(buf) + b)
                                     : floatx4{0.f, 0.f, 0.f, 0.f};
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(intx4, v), rs,
-                                               b < BYTES ? (int)(px0 * K * 4) + b : (int)PM_OOB, 0, 0);
+                                               b < BYTES ? (int)(px0 * K * 4) + b : (int)PM_OOB, 0, NTS ? 2 : 0);
       }
     } else {
 #pragma unroll
@@ -1015,6 +1016,7 @@ constexpr int PM_DIRECT_WPC = 8;  // waves per CU (AUTO)
 struct DirectOpts {
   int wpc = PM_DIRECT_WPC;  // waves per CU
   int gens = 1;             // launch generations (consecutive launches over equal run ranges)
+  bool nts = false;         // non-temporal burst stores (pixel-major)
 };
 
 template <int K, typename T, int LAYOUT, int NS>
@@ -1024,6 +1026,8 @@ int launch_direct_t(const PmArgs& a, const DirectOpts& o) {
   if (ngrp >= ((int64_t)1 << 31) - 4096 || a.P * K * 4 >= ((int64_t)1 << 31))
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: P too large");
   auto kern = fit_pm_direct<K, T, LAYOUT, NS, D>;
+  if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR)
+    if (o.nts) kern = fit_pm_direct<K, T, LAYOUT, NS, D, true>;
   const size_t lds = (size_t)4 * RPX * K * sizeof(float);  // 4 waves per workgroup
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
@@ -1165,8 +1169,9 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
   }
   if (dma_ok && sel == RTI_KERNEL_AUTO && N % 4 == 0 && pm_direct_ns(N)) {
     DirectOpts o;  // straight to registers.  Measurement flags: TILE_WAVES(w) waves per CU, CHUNKS(n) launch
-    if (w_req) o.wpc = w_req;  // generations
+    if (w_req) o.wpc = w_req;  // generations, NT_STORE non-temporal bursts
     if (c_req) o.gens = c_req;
+    o.nts = (kernel & RTI_KERNEL_NT_STORE) != 0;
     const int st = in_dtype == RTI_F32 ? launch_direct<float>(a, o) : launch_direct<int32_t>(a, o);
     return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
   }

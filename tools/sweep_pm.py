@@ -65,8 +65,10 @@ def main():
             variants.append((f"pm_block_{plan % 100000000 // 1000}px_w{plan % 1000}",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="tile", flags=fl)))
     direct = [(f"pm_direct_{w}wpc", w << L.RTI_KERNEL_TILE_WAVES_SHIFT) for w in (4, 8, 12)]
-    direct += [(f"pm_direct_gens{g}", g << L.RTI_KERNEL_CHUNKS_SHIFT) for g in (2, 4, 6)]
+    direct += [(f"pm_direct_gens{g}", g << L.RTI_KERNEL_CHUNKS_SHIFT) for g in (2, 4)]
+    direct += [("pm_direct_nts", L.RTI_KERNEL_NT_STORE), ("pm_direct_nts_12wpc", L.RTI_KERNEL_NT_STORE | (12 << 24))]
     for name, fl in direct:
+        fl |= L.RTI_KERNEL_STAGE  # the direct form for every k
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
         if plan // 100000000 == L.RTI_PM_DIRECT:
             variants.append((name, lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
@@ -81,7 +83,7 @@ def main():
         variants.append(("pm_valu_sgpr_weights", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
                                                                                  flags=L.RTI_KERNEL_PINV_LDS)))
     if k <= 9:  # measurement variants of the VALU stream: no stores / no arithmetic
-        st = L.RTI_KERNEL_STAGE
+        st = 0
         variants.append(("pm_valu_nostores", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
                                                                               flags=st | L.RTI_KERNEL_ONE_LAUNCH)))
         variants.append(("pm_valu_noarith", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
