@@ -158,18 +158,20 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int TP16 = 128;  // pixels per workgroup tile (4 blocks of 32)
 constexpr int KSMAX = 8;   // k-steps (16 lights each) the pipelined sweep holds in registers: N <= 128
 
-// NTS: non-temporal table stores (AUTO; false = plain stores, a measurement variant: RTI_OP_PLAIN_STORES=1)
-template <typename T, typename TO, bool VEC, bool NTS = true>
+// NTS: non-temporal table stores (AUTO; false = plain stores, a measurement variant: RTI_OP_PLAIN_STORES=1);
+// NBLK: 32-pixel blocks per workgroup tile (4: 128 pixels, AUTO; 8: 256, RTI_OP_TILE=256, a measurement variant)
+template <typename T, typename TO, bool VEC, bool NTS = true, int NBLK = 4>
 __global__ void __launch_bounds__(256)
 apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int E, int N,
               const T* __restrict__ I, int64_t P, int64_t lstride, int64_t cstride, TO* __restrict__ out,
               int64_t orow, int64_t ocs) {
   constexpr bool EXACT = std::is_same<T, uint8_t>::value;  // 0..255: exact in fp16, t = 1
-  extern __shared__ __attribute__((aligned(16))) _Float16 sI[];  // [2][TP16][KPITCH]
+  constexpr int TP = 32 * NBLK;  // pixels per workgroup tile
+  extern __shared__ __attribute__((aligned(16))) _Float16 sI[];  // [2][TP][KPITCH]
   __shared__ float s_red[4];
   const int KPITCH = Kp + 8;  // 16-B pad between pixel rows
-  _Float16* sIlo = sI + TP16 * KPITCH;
-  const int64_t p0 = (int64_t)blockIdx.x * TP16;
+  _Float16* sIlo = sI + TP * KPITCH;
+  const int64_t p0 = (int64_t)blockIdx.x * TP;
   const T* __restrict__ src = I + (int64_t)blockIdx.z * cstride;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
@@ -195,9 +197,9 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
   float t = 1.f;
   if constexpr (!EXACT) {
     float m = 0.f;
-    for (int idx = threadIdx.x; idx < N * (TP16 / 4); idx += 256) {
+    for (int idx = threadIdx.x; idx < N * (TP / 4); idx += 256) {
       float v[4];
-      load4(idx / (TP16 / 4), idx % (TP16 / 4), v);
+      load4(idx / (TP / 4), idx % (TP / 4), v);
 #pragma unroll
       for (int c = 0; c < 4; ++c) m = fmaxf(m, fabsf(v[c]) < INFINITY ? fabsf(v[c]) : 0.f);
     }
@@ -214,8 +216,8 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
     t = ldexpf(1.f, -e);
   }
   int need_lo = 0;
-  for (int idx = threadIdx.x; idx < Kp * (TP16 / 4); idx += 256) {
-    const int n = idx / (TP16 / 4), q4 = idx % (TP16 / 4);
+  for (int idx = threadIdx.x; idx < Kp * (TP / 4); idx += 256) {
+    const int n = idx / (TP / 4), q4 = idx % (TP / 4);
     float v[4];
     load4(n, q4, v);
 #pragma unroll
@@ -253,16 +255,16 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
       al[s] = *reinterpret_cast<const half8*>(olo + rowoff + 16 * ss);
     }
   };
-  auto mfma_block = [&](floatx16 (&acc)[4], const half8& a_hi, const half8& a_lo, int k0) {
+  auto mfma_block = [&](floatx16 (&acc)[NBLK], const half8& a_hi, const half8& a_lo, int k0) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < NBLK; ++b) {
       const half8 bh = *reinterpret_cast<const half8*>(sI + (32 * b + r) * KPITCH + k0 + 8 * h);
       acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_hi, bh, acc[b], 0, 0, 0);
       acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_lo, bh, acc[b], 0, 0, 0);
     }
     if (!EXACT && need_lo) {
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
+      for (int b = 0; b < NBLK; ++b) {
         const half8 bl = *reinterpret_cast<const half8*>(sIlo + (32 * b + r) * KPITCH + k0 + 8 * h);
         acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_hi, bl, acc[b], 0, 0, 0);
       }
@@ -272,7 +274,7 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
   // reg outer, pixel block inner: consecutive stores continue the same output row
   // (4 × 128 B = 512 B contiguous per row), which keeps HBM write pages open.
   // Non-temporal: the E×P output streams past the operator, which stays in L2.
-  auto store_block = [&](const floatx16 (&acc)[4], int rb, bool guard) {
+  auto store_block = [&](const floatx16 (&acc)[NBLK], int rb, bool guard) {
     // lane base: row rb*32 + 4h, pixel p0 + r; the 16 row offsets are wave-uniform multiples of orow
     TO* __restrict__ lb = dst + (int64_t)(rb * 32 + 4 * h) * orow + p0 + r;
 #pragma unroll
@@ -281,7 +283,7 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
       const int row = rb * 32 + dr + 4 * h;
       TO* __restrict__ rp = lb + (int64_t)dr * orow;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
+      for (int b = 0; b < NBLK; ++b) {
         if (!guard || (row < E && p0 + 32 * b + r < P)) {
           if constexpr (NTS)
             __builtin_nontemporal_store(cvt_out<TO>(acc[b][reg] * oscale), rp + 32 * b);
@@ -291,16 +293,16 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
       }
     }
   };
-  auto zero = [](floatx16 (&acc)[4]) {
+  auto zero = [](floatx16 (&acc)[NBLK]) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < NBLK; ++b)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[b][i] = 0.f;
   };
 
   int rb = rb0;
   const int nfull = E / 32;  // row blocks with all 32 rows in range
-  if (ksteps <= KSMAX && p0 + TP16 <= P && rb < nfull) {
+  if (ksteps <= KSMAX && p0 + TP <= P && rb < nfull) {
     // Software-pipelined sweep over whole row blocks of a whole pixel tile.  The next block's
     // operator rows are loaded BEFORE this block's 64 stores are issued: CDNA's single vmcnt
     // counter retires loads and stores in order, so a load issued after the stores cannot be
@@ -310,7 +312,7 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
     // first block is peeled, so the loop header sees the same outstanding-op pattern (16 loads
     // then 64 stores) from both edges and the compiler's waits stop at the loads.
     half8 ah[KSMAX], al[KSMAX];
-    floatx16 acc[4];
+    floatx16 acc[NBLK];
     load_a(rb, ah, al);
     zero(acc);
 #pragma unroll
@@ -339,7 +341,7 @@ apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int
     const bool aok = arow < E;
     const _Float16* ah = ohi + (int64_t)(aok ? arow : 0) * Kp + 8 * h;
     const _Float16* al = olo + (int64_t)(aok ? arow : 0) * Kp + 8 * h;
-    floatx16 acc[4];
+    floatx16 acc[NBLK];
     zero(acc);
     for (int k0 = 0; k0 < Kp; k0 += 16) {
       half8 a_hi = *reinterpret_cast<const half8*>(ah + k0);
@@ -358,8 +360,11 @@ template <typename T, typename TO>
 int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int E, int N, const void* I, int64_t P,
                int C, int64_t ls, int64_t cs, void* out, int64_t orow, int64_t ocs, bool vec, hipStream_t s) {
   constexpr bool EXACT = std::is_same<T, uint8_t>::value;
-  const size_t lds = (size_t)(EXACT ? 1 : 2) * TP16 * (Kp + 8) * sizeof(_Float16);
-  const unsigned gx = (unsigned)((P + TP16 - 1) / TP16);
+  const char* te = getenv("RTI_OP_TILE");  // measurement: 256-pixel tiles
+  const bool wide = vec && te && atoi(te) == 256;
+  const int tp = wide ? 256 : TP16;
+  const size_t lds = (size_t)(EXACT ? 1 : 2) * tp * (Kp + 8) * sizeof(_Float16);
+  const unsigned gx = (unsigned)((P + tp - 1) / tp);
   const int nwb = (E + 127) / 128;  // 4 waves × 32-row blocks per sweep step
   // E-split: one sweep over all row blocks per pixel tile once the tiles alone give two workgroups per CU
   // (c7 400²×100 → 10⁴ tables, 1250 tiles: 1.302 ms against 1.424 ms split in 2 and 1.549 in 3,
@@ -372,6 +377,7 @@ int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int 
   const char* ps = getenv("RTI_OP_PLAIN_STORES");  // measurement
   auto k = vec ? apply_op_f16s<T, TO, true> : apply_op_f16s<T, TO, false>;
   if (vec && ps && atoi(ps)) k = apply_op_f16s<T, TO, true, false>;
+  if (wide) k = apply_op_f16s<T, TO, true, true, 8>;
   if (lds > 65536 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
           hipSuccess)

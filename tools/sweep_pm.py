@@ -65,7 +65,8 @@ def main():
             variants.append((f"pm_block_{plan % 100000000 // 1000}px_w{plan % 1000}",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="tile", flags=fl)))
     direct = [(f"pm_direct_{w}wpc", w << L.RTI_KERNEL_TILE_WAVES_SHIFT) for w in (4, 8, 12)]
-    direct += [(f"pm_direct_gens{g}", g << L.RTI_KERNEL_CHUNKS_SHIFT) for g in (2, 4)]
+    direct += [(f"pm_direct_gens{g}", g << L.RTI_KERNEL_CHUNKS_SHIFT) for g in (2, 4, 6, 11, 15)]
+    direct += [(f"pm_direct_gens{g}_12wpc", (g << L.RTI_KERNEL_CHUNKS_SHIFT) | (12 << 24)) for g in (7, 14)]
     direct += [("pm_direct_nts", L.RTI_KERNEL_NT_STORE), ("pm_direct_nts_12wpc", L.RTI_KERNEL_NT_STORE | (12 << 24))]
     for name, fl in direct:
         fl |= L.RTI_KERNEL_STAGE  # the direct form for every k
