@@ -159,7 +159,8 @@ constexpr int TP16 = 128;  // pixels per workgroup tile (4 blocks of 32)
 constexpr int KSMAX = 8;   // k-steps (16 lights each) the pipelined sweep holds in registers: N <= 128
 
 // NTS: non-temporal table stores (AUTO; false = plain stores, a measurement variant: RTI_OP_PLAIN_STORES=1);
-// NBLK: 32-pixel blocks per workgroup tile (4: 128 pixels, AUTO; 8: 256, RTI_OP_TILE=256, a measurement variant)
+// NBLK: 32-pixel blocks per workgroup tile (4: 128 pixels; r04 measured 8 = 256 pixels at one wave per SIMD,
+// 1.47 against 1.31 ms on c7, profiles/r04v_c7_tile_sweep.log)
 template <typename T, typename TO, bool VEC, bool NTS = true, int NBLK = 4>
 __global__ void __launch_bounds__(256)
 apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int E, int N,
@@ -360,9 +361,7 @@ template <typename T, typename TO>
 int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int E, int N, const void* I, int64_t P,
                int C, int64_t ls, int64_t cs, void* out, int64_t orow, int64_t ocs, bool vec, hipStream_t s) {
   constexpr bool EXACT = std::is_same<T, uint8_t>::value;
-  const char* te = getenv("RTI_OP_TILE");  // measurement: 256-pixel tiles
-  const bool wide = vec && te && atoi(te) == 256;
-  const int tp = wide ? 256 : TP16;
+  const int tp = TP16;
   const size_t lds = (size_t)(EXACT ? 1 : 2) * tp * (Kp + 8) * sizeof(_Float16);
   const unsigned gx = (unsigned)((P + tp - 1) / tp);
   const int nwb = (E + 127) / 128;  // 4 waves × 32-row blocks per sweep step
@@ -377,7 +376,6 @@ int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int 
   const char* ps = getenv("RTI_OP_PLAIN_STORES");  // measurement
   auto k = vec ? apply_op_f16s<T, TO, true> : apply_op_f16s<T, TO, false>;
   if (vec && ps && atoi(ps)) k = apply_op_f16s<T, TO, true, false>;
-  if (wide) k = apply_op_f16s<T, TO, true, true, 8>;
   if (lds > 65536 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
           hipSuccess)

@@ -37,6 +37,17 @@ def test_stub_ptm_fit_and_residual(cuda):
     assert np.isfinite(rms) and res.shape == I.shape[1:]
 
 
+def test_stub_ptm_fit_pixel_major(cuda):
+    """The reference's own (R, R, N) stack handed to rti_fit_shared_pm by the stub, no transpose."""
+    ns = _stub_namespace()
+    d = golden("ptm_shared_256x256_N20.npz")
+    Ipm = torch.as_tensor(np.ascontiguousarray(np.moveaxis(d["I"], 0, -1)).astype(np.float32), device=cuda)
+    pv = torch.as_tensor(rti.pinv(d["lu"], d["lv"], "ptm").astype(np.float32), device=cuda)
+    coef = ns["ptm_fit_pixel_major"](Ipm, pv).cpu().numpy()
+    err, ok = coef_close(coef.reshape(-1, 6), d["coef"].reshape(-1, 6))
+    assert ok, err
+
+
 def test_stub_ptm_fit_u8(cuda):
     ns = _stub_namespace()
     d = golden("ptm_shared_256x256_N20.npz")

@@ -33,15 +33,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
     variants = args.gy.split(",")
 
-    def run(v):  # "auto", a grid.y, "plain" (plain instead of non-temporal table stores) or "tile256"
+    def run(v):  # "auto", a grid.y, or "plain" (plain instead of non-temporal table stores)
         os.environ.pop("RTI_OP_PLAIN_STORES", None)
-        os.environ.pop("RTI_OP_TILE", None)
-        if v in ("auto", "plain", "tile256"):
+        if v in ("auto", "plain"):
             os.environ.pop("RTI_OP_GY", None)
             if v == "plain":
                 os.environ["RTI_OP_PLAIN_STORES"] = "1"
-            if v == "tile256":
-                os.environ["RTI_OP_TILE"] = "256"
         else:
             os.environ["RTI_OP_GY"] = v
         wl.step(0)
