@@ -403,13 +403,11 @@ fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
 }
 
 // VALU streaming form (AUTO for k <= 9): the same units, interleaving and LDS ring as fit_pm_stream, but the
-// ring is consumed GPB·16 pixels (GPB groups of the stream) at a time: with GPB = 4 ONE PIXEL PER LANE, with
-// GPB = 2 (RTI_KERNEL_CHUNKS(2), N % 4 == 0) two lanes per pixel, lanes 32.. taking the upper part of the
-// lights and a cross-half add at the end — half the ring per wave, so twice the waves fit the LDS.  A lane
-// reads its pixel's row from the ring (ds_read_b128, 4 lights) and accumulates k coefficients with packed FMAs
-// (v_pk_fma_f32 over light pairs: acc_i.xy += I[n, n+1]·pinv[i][n, n+1], the weights broadcast from an LDS
-// copy), so a pixel·light costs k/2 VALU lane-ops instead of the 16 MACs a 16x16x4 MFMA spends on it
-// whatever k (PTM-6: 10 of 16 matrix rows idle).  The lanes of a block may belong to different
+// ring is consumed 64 pixels (4 groups of the stream) at a time with ONE PIXEL PER LANE: lane l reads its
+// pixel's row from the ring (ds_read_b128, 4 lights) and accumulates k coefficients with packed FMAs
+// (v_pk_fma_f32 over light pairs: acc_i.xy += I[n, n+1]·pinv[i][n, n+1], the weights wave-uniform in SGPRs,
+// read by scalar loads), so a pixel·light costs k/2 VALU lane-ops instead of the 16 MACs a 16x16x4 MFMA
+// spends on it whatever k (PTM-6: 10 of 16 matrix rows idle).  The lanes of a block may belong to different
 // units and channels: each lane keeps its own group cursor, and the coefficients leave by buffer stores
 // over the WHOLE coefficient array (per-lane 32-bit offsets; lanes past P or past the stream get an
 // out-of-range offset), so every block issues the same SB stores.
@@ -418,9 +416,7 @@ fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
 // steps by wave-uniform scalar loads into SGPRs (RTI_KERNEL_PINV_LDS's opposite, a measurement variant) instead
 // of broadcast ds_read_b128 from the LDS copy: 0.667 against 0.633 ms on c3 (profiles/r04s_pm_sweep_c3.log) —
 // the scalar loads return out of order, so each half step waits on lgkmcnt(0)
-// BURST (pixel-major, k even): the coefficients of BURST consecutive blocks wait in registers and leave as one
-// burst of BURST·k/2 stores (measurement: RTI_KERNEL_TILE_DEPTH(BURST))
-template <int K, typename T, int LAYOUT, int ALIGN, int MODE = 0, int GPB = 4, int BURST = 1>
+template <int K, typename T, int LAYOUT, int ALIGN, int MODE = 0>
 __global__ void __launch_bounds__(512)
 fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
                float* __restrict__ coef, int64_t ocstride, int C, int U, int nu, int64_t tu, int ring,
@@ -448,9 +444,7 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
   if (nk == 0) return;
   const int ust = (int)GW;
   const int ng = (int)(nk * U);                  // groups of the stream
-  static_assert(GPB == 4 || (GPB == 2 && ALIGN == 4), "two lanes per pixel need 16-byte rows");
-  constexpr int BPX = 16 * GPB;                   // pixels per block
-  const int nb = (ng + GPB - 1) / GPB;            // blocks
+  const int nb = (ng + 3) >> 2;                   // 64-pixel blocks
   const int dt = (int)(nk * ((U * GBY) >> 10));  // DMAs of the stream
   int cd = (int)(gw / nu), ud = (int)(gw - (int64_t)cd * nu);
   const int UB = U * GBY, UKB = UB >> 10;
@@ -480,10 +474,8 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
   };
   int issued = dt < slots ? dt : slots;
   for (int d = 0; d < issued; ++d) issue();
-  // the lane's pixel in a block, and for GPB = 2 the half of the lights it takes
-  const int pxl = lane & (BPX - 1), half = GPB == 2 ? lane >> 5 : 0;
-  // the lane's group cursor: stream group j = GPB·b + (pxl >> 4) -> unit (lc, lu), group gi within it
-  int lc = (int)(gw / nu), lu = (int)(gw - (int64_t)lc * nu), gi = pxl >> 4;  // (the prologue moved cd, ud)
+  // the lane's group cursor: stream group j = 4b + (lane >> 4) -> unit (lc, lu), group gi within it
+  int lc = (int)(gw / nu), lu = (int)(gw - (int64_t)lc * nu), gi = lane >> 4;  // (the prologue moved cd, ud)
   {
     while (gi >= U) {
       gi -= U;
@@ -497,29 +489,14 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
   const int q = lane & 15;
   __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef, (short)0, (int)coef_bytes, 0x00020000);
   int base = 0, gd = -1;
-  const int lrow = N * (int)sizeof(T) * pxl;  // the lane's row inside a block
-  float bst[BURST][K];
-  uint32_t boff[BURST];
-  auto flush = [&](int last) {  // the newest `last` entries of the shift register (wave-uniform)
-#pragma unroll
-    for (int r = 0; r < BURST; ++r)
-      if (r >= BURST - last)
-#pragma unroll
-        for (int i = 0; i < K; i += 2) {
-          const uint32_t off = boff[r] == PM_OOB_ALL ? PM_OOB_ALL : boff[r] + 4 * i;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(intx2, f2{bst[r][i], bst[r][i + 1]}), rs, off,
-                                                0, 0);
-        }
-  };
+  const int lrow = N * (int)sizeof(T) * lane;  // the lane's row inside a block
   for (int b = 0; b < nb; ++b) {
-    const int gend_b = GPB * (b + 1) < ng ? GPB * (b + 1) : ng;
+    const int gend_b = 4 * (b + 1) < ng ? 4 * (b + 1) : ng;
     const int end = GBY * gend_b;
     const int dn = ((end + 1023) >> 10) - 1;
-    // the refill after block g issues DMAs up to (GBY·min(GPB(g+1), ng) + ring)/1 KiB (prologue: ring/1 KiB)
-    while (((GBY * (GPB * (gd + 1) < ng ? GPB * (gd + 1) : ng) + ring) >> 10) < dn + 1) ++gd;
-    // stores issued after DMA dn: those of blocks gd + 1 .. b − 1 (in bursts of BURST blocks at blocks
-    // BURST − 1, 2·BURST − 1, ...)
-    const int nwait = (issued - 1 - dn) + SB * BURST * (b / BURST - (gd + 1) / BURST);
+    // the refill after block g issues DMAs up to (GBY·min(4(g+1), ng) + ring)/1 KiB (prologue: ring/1 KiB)
+    while (((GBY * (4 * (gd + 1) < ng ? 4 * (gd + 1) : ng) + ring) >> 10) < dn + 1) ++gd;
+    const int nwait = (issued - 1 - dn) + SB * (b - 1 - gd);
     wait_vm_dyn(nwait > 63 ? 63 : nwait);
     int a0 = base + lrow;
     a0 -= a0 >= ring ? ring : 0;
@@ -533,16 +510,10 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
     if constexpr (ALIGN == 4 && MODE != 2) {
       // one step of 4 lights ahead: step n + 4's row values and weights are read (LDS: in order, counted
       // waits) while step n's 2·K packed FMAs issue
-      // GPB = 2: lanes 0..31 take lights [0, NH), lanes 32..63 [NH, N) (NH a multiple of 4, the upper part the
-      // longer one); a lower-half step past NH reads zeros
-      const int NH = GPB == 2 ? (N >> 3) << 2 : 0, nofs = half ? NH : 0;
       auto rdx = [&](int nn) {
-        int a = a0 + (nofs + nn) * (int)sizeof(T);
+        int a = a0 + nn * (int)sizeof(T);
         a -= a >= ring ? ring : 0;
-        const floatx4 v = lds4<4, T>(reinterpret_cast<const float*>(rp + a), 0);
-        if constexpr (GPB == 2)  // the lower half past NH: zeros (the bytes there belong to the upper half)
-          return (half || nn < NH) ? v : floatx4{0.f, 0.f, 0.f, 0.f};
-        return v;
+        return lds4<4, T>(reinterpret_cast<const float*>(rp + a), 0);
       };
       auto step = [&](const floatx4& x, const floatx4 (&w)[K]) {
         const f2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]};
@@ -552,12 +523,12 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
           acc[i] = x23 * f2{w[i][2], w[i][3]} + acc[i];
         }
       };
-      const int n4 = GPB == 2 ? N - NH : (N & ~3);
+      const int n4 = N & ~3;
       if (n4 > 0) {
         // weights pinv[i][n .. n+3]: broadcast reads of the LDS copy, or scalar loads into SGPRs (MODE 3)
         auto wts = [&](int nn, int i) {
-          return MODE == 3 ? *reinterpret_cast<const floatx4*>(pinv + i * N + nofs + nn)
-                           : *reinterpret_cast<const floatx4*>(lw + (nofs + nn) * K + 4 * i);
+          return MODE == 3 ? *reinterpret_cast<const floatx4*>(pinv + i * N + nn)
+                           : *reinterpret_cast<const floatx4*>(lw + nn * K + 4 * i);
         };
         // ping-pong register sets (no loop-carried copies): each half issues the next step's loads, then the
         // FMAs of the step loaded one half earlier (scalar loads return out of order, so the only wait, at the
@@ -584,7 +555,7 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
           __builtin_amdgcn_sched_barrier(0);
           step(xb, wb);
         }
-        n = GPB == 2 ? N : n4;
+        n = n4;
       }
     }
     for (; n < N; ++n) {  // N % 4 (or every light when the rows are not 16-byte aligned)
@@ -597,10 +568,6 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
     float c[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) c[i] = (acc[i][0] + acc[i][1]) + acc1[i];
-    if constexpr (GPB == 2) {  // the two halves of each pixel's sum (lanes l and l + 32)
-#pragma unroll
-      for (int i = 0; i < K; ++i) c[i] += __shfl_xor(c[i], 32);
-    }
     if constexpr (MODE == 1) {  // measurement: keep the arithmetic, drop the stores
       float t = 0.f;
 #pragma unroll
@@ -610,21 +577,9 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
     {
     // stores: pixel px of channel lc; lanes past the stream or past P drop theirs
     const int px = (lu * U + gi) * 16 + q;
-    const bool ok = GPB * b + (pxl >> 4) < ng && px < P && half == 0;
+    const bool ok = 4 * b + (lane >> 4) < ng && px < P;
     const uint32_t cb = (uint32_t)((int64_t)lc * ocstride * 4);
-    if constexpr (BURST > 1) {
-      static_assert(LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0, "bursts: pixel-major, k even");
-#pragma unroll
-      for (int r = 0; r + 1 < BURST; ++r) {  // shift register of the last BURST blocks' coefficients
-#pragma unroll
-        for (int i = 0; i < K; ++i) bst[r][i] = bst[r + 1][i];
-        boff[r] = boff[r + 1];
-      }
-#pragma unroll
-      for (int i = 0; i < K; ++i) bst[BURST - 1][i] = c[i];
-      boff[BURST - 1] = ok ? cb + (uint32_t)(px * K * 4) : PM_OOB_ALL;
-      if (b % BURST == BURST - 1) flush(BURST);
-    } else if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0) {
+    if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0) {
 #pragma unroll
       for (int i = 0; i < K; i += 2) {
         const uint32_t off = ok ? cb + (uint32_t)((px * K + i) * 4) : PM_OOB_ALL;
@@ -643,9 +598,9 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
     const int lim0 = (end + ring) >> 10;
     const int lim = lim0 < dt ? lim0 : dt;
     for (; issued < lim; ++issued) issue();
-    base += GPB * GBY;
+    base += 4 * GBY;
     base -= base >= ring ? ring : 0;
-    gi += GPB;  // the lane's next group: GPB further along the stream
+    gi += 4;  // the lane's next group: 4 further along the stream
     while (gi >= U) {
       gi -= U;
       lu += ust;
@@ -655,8 +610,6 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
       }
     }
   }
-  if constexpr (BURST > 1 && MODE != 1)
-    if (nb % BURST) flush(nb % BURST);
 }
 
 // DIRECT form (AUTO for N % 4 == 0, N <= 256): the stack goes straight into VGPRs, LDS only stages the
@@ -988,25 +941,29 @@ int launch_stream(const PmArgs& a, const StreamPlan& pl) {
 }
 
 // VALU stream (k <= 9): one workgroup of W waves per CU (W <= 6), a ring per wave that holds a 64-pixel block
-// (4 groups) + 1 KiB; AUTO takes the most waves that fit (6 up to N = 100 for 4-byte values, 4 up to 150)
+// (4 groups) + 1 KiB; AUTO takes the most waves that fit (6 up to N = 100 for 4-byte values, 4 up to 150).
+// Measured and not kept (profiles/r04w-r04y_pm_sweep_c3*.log, c3 against 0.627–0.635 ms for this form): two
+// lanes per pixel at 8 waves 0.628–0.631, the coefficients of 4–8 blocks held in registers and stored as
+// one burst 0.649–0.657, launch generations with the coefficients staged in LDS and written at each
+// launch's end 0.91–1.01 (the minimum rings starve the stream).  Without its stores this form runs 0.50 ms
+// (RTI_KERNEL_ONE_LAUNCH): the reads and arithmetic are at the light-major fit's speed, the spread stores are
+// what costs.
 struct VPlan {
-  int W = 0, ring = 0, gpb = 4, burst = 1;
+  int W = 0, ring = 0;
   size_t lds = 0;
 };
 
-// gpb: groups per block (4: a pixel per lane; 2: two lanes per pixel, N % 4 == 0 and 4-byte values only)
-VPlan vstream_plan(int k, int N, size_t es, int w_req, int gpb = 4) {
-  if (k > 9 || (gpb == 2 && (N % 4 || N < 8 || es != 4))) return VPlan();
-  const int64_t need = (int64_t)gpb * 16 * N * es + 1024;
+VPlan vstream_plan(int k, int N, size_t es, int w_req) {
+  if (k > 9) return VPlan();
+  const int64_t need = (int64_t)4 * 16 * N * es + 1024;
   const size_t op = (size_t)((N + 3) & ~3) * (k <= 6 ? 6 : 9) * sizeof(float);
-  for (int W : {8, 6, 5, 4, 3, 2, 1}) {
+  for (int W : {6, 5, 4, 3, 2, 1}) {
     if (w_req && W != w_req) continue;
     const int ring = (int)(((PM_LDS - op) / W) >> 10 << 10);
     if (ring < need) continue;
     VPlan pl;
     pl.W = W;
     pl.ring = ring;
-    pl.gpb = gpb;
     pl.lds = op + (size_t)W * ring;
     return pl;
   }
@@ -1019,14 +976,6 @@ int launch_vstream_t(const PmArgs& a, const VPlan& pl) {
               : a.mode == 2 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 2>
               : a.mode == 3 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 3>
                             : fit_pm_vstream<K, T, LAYOUT, ALIGN, 0>;
-  if constexpr (ALIGN == 4)
-    if (pl.gpb == 2) kern = fit_pm_vstream<K, T, LAYOUT, ALIGN, 0, 2>;
-  if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0) {
-    if (pl.burst == 4) kern = pl.gpb == 2 && ALIGN == 4 ? fit_pm_vstream<K, T, LAYOUT, 4, 0, 2, 4>
-                                                        : fit_pm_vstream<K, T, LAYOUT, ALIGN, 0, 4, 4>;
-    if (pl.burst == 8) kern = pl.gpb == 2 && ALIGN == 4 ? fit_pm_vstream<K, T, LAYOUT, 4, 0, 2, 8>
-                                                        : fit_pm_vstream<K, T, LAYOUT, ALIGN, 0, 4, 8>;
-  }
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)pl.lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
@@ -1166,7 +1115,7 @@ extern "C" int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int
   const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
   const bool stage = (kernel & RTI_KERNEL_STAGE) != 0;
   if ((kernel & 0xff) == RTI_KERNEL_AUTO && !stage) {
-    const VPlan vp = vstream_plan(k, N, 4, w_req, c_req == 2 ? 2 : 4);
+    const VPlan vp = vstream_plan(k, N, 4, w_req);
     if (vp.W && (int64_t)C * P * k * 4 < 0xFFFFFFF0ll) return RTI_PM_VALU_STREAM * 100000000 + (vp.ring >> 10) * 1000 + vp.W;
   }
   if ((kernel & 0xff) == RTI_KERNEL_AUTO && N % 4 == 0 && pm_direct_ns(N))
@@ -1218,8 +1167,7 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
   // the direct form (c4 3.754 against 3.858 ms for the MFMA stream; profiles/r04r_pm_sweep_c*.log);
   // RTI_KERNEL_STAGE with AUTO forces the direct form (its coefficients are staged through LDS)
   if (dma_ok && sel == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE)) {
-    VPlan vp = vstream_plan(k, N, es, w_req, c_req == 2 ? 2 : 4);  // RTI_KERNEL_CHUNKS(2): two lanes per pixel
-    vp.burst = (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF;            // RTI_KERNEL_TILE_DEPTH(4|8): store bursts
+    const VPlan vp = vstream_plan(k, N, es, w_req);
     if (vp.W && vstream_coef_ok(a)) {
       const int st = in_dtype == RTI_F32 ? launch_vstream<float>(a, vp) : launch_vstream<int32_t>(a, vp);
       return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");

@@ -73,12 +73,11 @@ def main():
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
         if plan // 100000000 == L.RTI_PM_DIRECT:
             variants.append((name, lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
-    for w, g, bu in ((6, 0, 0), (4, 0, 0), (8, 2, 0), (6, 0, 4), (6, 0, 8), (4, 0, 8), (8, 2, 4), (8, 2, 8)):
-        # g = 2: two lanes per pixel; bu: store bursts of bu blocks
-        fl = (w << L.RTI_KERNEL_TILE_WAVES_SHIFT) | (g << L.RTI_KERNEL_CHUNKS_SHIFT) | (bu << L.RTI_KERNEL_TILE_DEPTH_SHIFT)
+    for w in (6, 5, 4):
+        fl = w << L.RTI_KERNEL_TILE_WAVES_SHIFT
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
         if plan // 100000000 == L.RTI_PM_VALU_STREAM:
-            variants.append((f"pm_valu{'2' if g else ''}_w{w}_burst{bu or 1}_ring{plan % 100000000 // 1000}K",
+            variants.append((f"pm_valu_w{w}_ring{plan % 100000000 // 1000}K",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
     variants.append(("pm_auto", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto")))
     if k <= 9:  # the VALU stream's weights by scalar loads (SGPRs) instead of the LDS copy
