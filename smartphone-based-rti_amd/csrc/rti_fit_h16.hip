@@ -89,8 +89,7 @@ __device__ __forceinline__ void h16_store(float* __restrict__ dst, int64_t P, in
   }
 }
 
-// DEPTH: steps of loads in flight (2: the step after next is loaded while this one is computed; 3: two ahead)
-template <int K, int LAYOUT, int R, int STEP, int DEPTH = 2>
+template <int K, int LAYOUT, int R, int STEP>
 __global__ void __launch_bounds__(64 * H16_W)
 fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __restrict__ I, int64_t pb, int64_t pe,
         int tpw, int64_t P, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
@@ -187,57 +186,33 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
   // a finished tile's stores are issued at the start of the next step, before that step's loads; sb holds
   // step s + 1, sa receives step s + 2.
   v4i sa[TL::NL], sb[TL::NL];
-  if constexpr (DEPTH == 2) {
-    load(0, sa);
-    load(S > 1 ? 1 : 0, sb);
+  load(0, sa);
+  load(S > 1 ? 1 : 0, sb);
+  park(0, sa);
+  __syncthreads();
+  const int S2 = S + (S & 1);
+  for (int s = 0; s < S2; s += 2) {
+    if (s > 0 && s % T == 0) finish(s / T - 1);
+    load(min(s + 2, S - 1), sa);
+    compute(0, s % T);
+    park(1, sb);
+    __syncthreads();
+    if (s + 1 < S && (s + 1) % T == 0) finish((s + 1) / T - 1);
+    load(min(s + 3, S - 1), sb);
+    if (s + 1 < S) compute(1, (s + 1) % T);
     park(0, sa);
     __syncthreads();
-    const int S2 = S + (S & 1);
-    for (int s = 0; s < S2; s += 2) {
-      if (s > 0 && s % T == 0) finish(s / T - 1);
-      load(min(s + 2, S - 1), sa);
-      compute(0, s % T);
-      park(1, sb);
-      __syncthreads();
-      if (s + 1 < S && (s + 1) % T == 0) finish((s + 1) / T - 1);
-      load(min(s + 3, S - 1), sb);
-      if (s + 1 < S) compute(1, (s + 1) % T);
-      park(0, sa);
-      __syncthreads();
-    }
-  } else {
-    // three register stages: step s in LDS buffer s & 1, steps s + 1 and s + 2 in registers, step s + 3
-    // loaded into the stage just parked; the stream is padded to whole triples (padding steps load step
-    // S − 1 again and are neither computed nor finished)
-    v4i sc[TL::NL];
-    load(0, sa);
-    load(min(1, S - 1), sb);
-    load(min(2, S - 1), sc);
-    park(0, sa);
-    __syncthreads();
-    auto stepx = [&](int st, v4i (&ld)[TL::NL], const v4i (&pk)[TL::NL]) {
-      if (st < S && st > 0 && st % T == 0) finish(st / T - 1);
-      load(min(st + 3, S - 1), ld);
-      if (st < S) compute(st & 1, st % T);
-      park((st + 1) & 1, pk);
-      __syncthreads();
-    };
-    for (int s = 0; s < S; s += 3) {
-      stepx(s, sa, sb);
-      stepx(s + 1, sb, sc);
-      stepx(s + 2, sc, sa);
-    }
   }
   finish(ntiles - 1);
 }
 
 template <int K, int LAYOUT, int R, int STEP>
 int launch_h16_t(const unsigned char* op, int N, const unsigned char* I, int64_t P, int C, int64_t ls, int64_t cs,
-                 float* coef, int64_t ocs, int tpw, int depth, hipStream_t s) {
+                 float* coef, int64_t ocs, int tpw, hipStream_t s) {
   const size_t lds = h16_lds_bytes<R, STEP>(N);
   if (lds > 160 * 1024)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_h16: LDS of %zu B (N=%d) exceeds 160 KiB", lds, N);
-  auto kern = depth == 3 ? fit_h16<K, LAYOUT, R, STEP, 3> : fit_h16<K, LAYOUT, R, STEP, 2>;
+  auto kern = fit_h16<K, LAYOUT, R, STEP>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_h16: cannot reserve %zu B of LDS", lds);
@@ -256,8 +231,7 @@ struct H16Args {
   int64_t ls, cs;
   float* coef;
   int64_t ocs;
-  int want;   // RTI_KERNEL_CHUNKS: tiles per workgroup (0 = AUTO)
-  int depth;  // RTI_KERNEL_TILE_DEPTH: steps of loads in flight (0 = AUTO = 2)
+  int want;  // RTI_KERNEL_CHUNKS: tiles per workgroup (0 = AUTO)
   hipStream_t s;
 };
 
@@ -267,8 +241,7 @@ int launch_h16_g(const H16Args& a) {
   const int64_t tpc = (a.P + R - 1) / R, cus = device_cus();
   const int64_t wpc = cus >= a.C ? cus / a.C : 1;
   const int tpw = a.want ? a.want : (int)((tpc + wpc - 1) / wpc);
-  return launch_h16_t<K, LAYOUT, R, STEP>(a.op, a.N, a.I, a.P, a.C, a.ls, a.cs, a.coef, a.ocs, tpw,
-                                          a.depth == 3 ? 3 : 2, a.s);
+  return launch_h16_t<K, LAYOUT, R, STEP>(a.op, a.N, a.I, a.P, a.C, a.ls, a.cs, a.coef, a.ocs, tpw, a.s);
 }
 
 template <int K>
@@ -345,11 +318,9 @@ extern "C" int rti_fit_shared_h16(const void* op, int k, int N, const uint8_t* I
   if (P % 16 || ls % 16 || cs % 16 || !aligned_to(I, 16) || !aligned_to(op, 16) || !aligned_to(coef, 16) || ocs % 4)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_h16: needs P, strides and pointers 16-byte aligned");
   note_launches(1);
-  // RTI_KERNEL_CHUNKS(n): tiles per workgroup = n, RTI_KERNEL_TILE_DEPTH(3): three steps of loads in flight
-  // (measurement)
+  // RTI_KERNEL_CHUNKS(n): tiles per workgroup = n (measurement)
   const H16Args a{static_cast<const unsigned char*>(op), N, I, P, C, ls, cs, coef, ocs,
-                  (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF,
-                  (hipStream_t)stream};
+                  (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, (hipStream_t)stream};
   switch (k) {
     case 6: return launch_h16_l<6>(coef_layout, a);
     case 9: return launch_h16_l<9>(coef_layout, a);

@@ -87,10 +87,7 @@ def test_auto_is_h16_and_matches_q8(cuda):
 def test_tile_streams_bit_identical(cuda):
     """AUTO lets every workgroup stream several interleaved 2048-pixel tiles through one load pipeline; the
     result equals one cold tile per workgroup (RTI_KERNEL_CHUNKS(1)) and 3 tiles per workgroup bit for bit
-    (ragged P: a partial last tile and a short last stream, 3 channels, HSH-16 and PTM-6), and so does the
-    three-stage load pipeline (RTI_KERNEL_TILE_DEPTH(3); N = 100 and 200: 4 and 7 steps per tile, streams that
-    end inside a triple)."""
-    D3 = 3 << L.RTI_KERNEL_TILE_DEPTH_SHIFT
+    (ragged P: a partial last tile and a short last stream, 3 channels, HSH-16 and PTM-6)."""
     for k, N in ((16, 200), (6, 100)):
         C, P = 3, 2048 * 1050 + 16 * 5
         lu, lv = o.synth_dirs(N, 4)
@@ -99,8 +96,7 @@ def test_tile_streams_bit_identical(cuda):
         g = torch.Generator(device=cuda).manual_seed(5)
         I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda, dtype=torch.uint8)
         outs = []
-        for flags in (0, 1 << L.RTI_KERNEL_CHUNKS_SHIFT, 3 << L.RTI_KERNEL_CHUNKS_SHIFT, D3,
-                      D3 | (1 << L.RTI_KERNEL_CHUNKS_SHIFT), D3 | (2 << L.RTI_KERNEL_CHUNKS_SHIFT)):
+        for flags in (0, 1 << L.RTI_KERNEL_CHUNKS_SHIFT, 3 << L.RTI_KERNEL_CHUNKS_SHIFT):
             coef = torch.full((C, P, k), float("nan"), device=cuda)
             rti.api.fit_h16_into(op, I, coef, k=k, flags=flags)
             outs.append(coef)

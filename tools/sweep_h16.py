@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The 8-bit shared fit (rti_fit_shared_h16) variants interleaved in ONE process, HIP events per launch, median
-of --rounds: load pipeline depth (RTI_KERNEL_TILE_DEPTH 2 / 3) and tiles per workgroup (RTI_KERNEL_CHUNKS),
-each checked bit-identical to the AUTO launch.
+of --rounds: tiles per workgroup (RTI_KERNEL_CHUNKS), each checked bit-identical to the AUTO launch.  (The
+r04 runs of this tool also timed a three-stage load pipeline, since removed: profiles/r04s_h16_depth_sweep_*.)
 
   python tools/sweep_h16.py --config c3|c4 [--rounds 20] [--tpw 0,8,16]
 """
@@ -39,9 +39,9 @@ def main():
     ref = torch.empty((C, P, k), device=dev)
     variants = []
     for tpw in [int(x) for x in args.tpw.split(",")]:
-        for depth in (2, 3):
-            fl = (tpw << L.RTI_KERNEL_CHUNKS_SHIFT) | (depth << L.RTI_KERNEL_TILE_DEPTH_SHIFT)
-            variants.append((f"h16_depth{depth}_tpw{tpw or 'auto'}",
+        for depth in (2,):
+            fl = tpw << L.RTI_KERNEL_CHUNKS_SHIFT
+            variants.append((f"h16_tpw{tpw or 'auto'}",
                              lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
     rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
     same = {}
