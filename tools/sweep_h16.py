@@ -39,10 +39,9 @@ def main():
     ref = torch.empty((C, P, k), device=dev)
     variants = []
     for tpw in [int(x) for x in args.tpw.split(",")]:
-        for depth in (2,):
-            fl = tpw << L.RTI_KERNEL_CHUNKS_SHIFT
-            variants.append((f"h16_tpw{tpw or 'auto'}",
-                             lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
+        fl = tpw << L.RTI_KERNEL_CHUNKS_SHIFT
+        variants.append((f"h16_tpw{tpw or 'auto'}",
+                         lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
     rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
     same = {}
     for name, fn in variants:
