@@ -89,7 +89,8 @@ __device__ __forceinline__ void h16_store(float* __restrict__ dst, int64_t P, in
   }
 }
 
-template <int K, int LAYOUT, int R, int STEP>
+// CB: 16-pixel groups whose reads and MFMAs are batched per step (AUTO 4; 1 one group at a time)
+template <int K, int LAYOUT, int R, int STEP, int CB = 1>
 __global__ void __launch_bounds__(64 * H16_W)
 fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __restrict__ I, int64_t pb, int64_t pe,
         int tpw, int64_t P, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
@@ -152,11 +153,31 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
     const unsigned char* tb = tile + b * (STEP * TL::RS) + roff;
     const half8 ah = *reinterpret_cast<const half8*>(lop + 2 * (arow + t * STEP));
     const half8 al = *reinterpret_cast<const half8*>(lop + h16_half_bytes(N) + 2 * (arow + t * STEP));
+    if constexpr (CB == 1) {
 #pragma unroll
-    for (int c = 0; c < TL::G; ++c) {
-      const half8 x = widen8(tr8(tb + 16 * c));
-      acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, x, acc[c], 0, 0, 0);
-      acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, x, acc[c], 0, 0, 0);
+      for (int c = 0; c < TL::G; ++c) {
+        const half8 x = widen8(tr8(tb + 16 * c));
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, x, acc[c], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, x, acc[c], 0, 0, 0);
+      }
+    } else {
+      // batches of CB groups: their transposed reads issued together, then the hi MFMAs of the batch, then the
+      // lo ones (each accumulator's two MFMAs CB apart instead of back to back)
+#pragma unroll
+      for (int c0 = 0; c0 < TL::G; c0 += CB) {
+        v2i raw[CB];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) raw[c] = tr8(tb + 16 * (c0 + c));
+        half8 x[CB];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) x[c] = widen8(raw[c]);
+#pragma unroll
+        for (int c = 0; c < CB; ++c)
+          acc[c0 + c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, x[c], acc[c0 + c], 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < CB; ++c)
+          acc[c0 + c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, x[c], acc[c0 + c], 0, 0, 0);
+      }
     }
   };
 
@@ -208,11 +229,13 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
 
 template <int K, int LAYOUT, int R, int STEP>
 int launch_h16_t(const unsigned char* op, int N, const unsigned char* I, int64_t P, int C, int64_t ls, int64_t cs,
-                 float* coef, int64_t ocs, int tpw, hipStream_t s) {
+                 float* coef, int64_t ocs, int tpw, int cb, hipStream_t s) {
   const size_t lds = h16_lds_bytes<R, STEP>(N);
   if (lds > 160 * 1024)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_h16: LDS of %zu B (N=%d) exceeds 160 KiB", lds, N);
-  auto kern = fit_h16<K, LAYOUT, R, STEP>;
+  // AUTO batches 4 groups per read/MFMA round (c2 u8 0.0379 against 0.0443 ms one group at a time, c3 / c4 u8
+  // within 1 %: profiles/r04z_h16_batch_sweep_c*.log); RTI_KERNEL_TILE_DEPTH(1|8) for measurement
+  auto kern = cb == 8 ? fit_h16<K, LAYOUT, R, STEP, 8> : cb == 1 ? fit_h16<K, LAYOUT, R, STEP, 1> : fit_h16<K, LAYOUT, R, STEP, 4>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_h16: cannot reserve %zu B of LDS", lds);
@@ -232,6 +255,7 @@ struct H16Args {
   float* coef;
   int64_t ocs;
   int want;  // RTI_KERNEL_CHUNKS: tiles per workgroup (0 = AUTO)
+  int cb;    // RTI_KERNEL_TILE_DEPTH: batched groups (measurement)
   hipStream_t s;
 };
 
@@ -241,7 +265,7 @@ int launch_h16_g(const H16Args& a) {
   const int64_t tpc = (a.P + R - 1) / R, cus = device_cus();
   const int64_t wpc = cus >= a.C ? cus / a.C : 1;
   const int tpw = a.want ? a.want : (int)((tpc + wpc - 1) / wpc);
-  return launch_h16_t<K, LAYOUT, R, STEP>(a.op, a.N, a.I, a.P, a.C, a.ls, a.cs, a.coef, a.ocs, tpw, a.s);
+  return launch_h16_t<K, LAYOUT, R, STEP>(a.op, a.N, a.I, a.P, a.C, a.ls, a.cs, a.coef, a.ocs, tpw, a.cb, a.s);
 }
 
 template <int K>
@@ -320,7 +344,8 @@ extern "C" int rti_fit_shared_h16(const void* op, int k, int N, const uint8_t* I
   note_launches(1);
   // RTI_KERNEL_CHUNKS(n): tiles per workgroup = n (measurement)
   const H16Args a{static_cast<const unsigned char*>(op), N, I, P, C, ls, cs, coef, ocs,
-                  (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, (hipStream_t)stream};
+                  (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF,
+                  (hipStream_t)stream};
   switch (k) {
     case 6: return launch_h16_l<6>(coef_layout, a);
     case 9: return launch_h16_l<9>(coef_layout, a);

@@ -96,7 +96,8 @@ def test_tile_streams_bit_identical(cuda):
         g = torch.Generator(device=cuda).manual_seed(5)
         I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda, dtype=torch.uint8)
         outs = []
-        for flags in (0, 1 << L.RTI_KERNEL_CHUNKS_SHIFT, 3 << L.RTI_KERNEL_CHUNKS_SHIFT):
+        for flags in (0, 1 << L.RTI_KERNEL_CHUNKS_SHIFT, 3 << L.RTI_KERNEL_CHUNKS_SHIFT,
+                      4 << L.RTI_KERNEL_TILE_DEPTH_SHIFT, 8 << L.RTI_KERNEL_TILE_DEPTH_SHIFT):  # batched groups
             coef = torch.full((C, P, k), float("nan"), device=cuda)
             rti.api.fit_h16_into(op, I, coef, k=k, flags=flags)
             outs.append(coef)

@@ -39,9 +39,10 @@ def main():
     ref = torch.empty((C, P, k), device=dev)
     variants = []
     for tpw in [int(x) for x in args.tpw.split(",")]:
-        fl = tpw << L.RTI_KERNEL_CHUNKS_SHIFT
-        variants.append((f"h16_tpw{tpw or 'auto'}",
-                         lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
+        for cb in (1, 4, 8):  # groups batched per step (RTI_KERNEL_TILE_DEPTH)
+            fl = (tpw << L.RTI_KERNEL_CHUNKS_SHIFT) | (cb << L.RTI_KERNEL_TILE_DEPTH_SHIFT)
+            variants.append((f"h16_tpw{tpw or 'auto'}_batch{cb}",
+                             lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
     rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
     same = {}
     for name, fn in variants:
