@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """The 8-bit shared fit (rti_fit_shared_h16) variants interleaved in ONE process, HIP events per launch, median
-of --rounds: tiles per workgroup (RTI_KERNEL_CHUNKS), each checked bit-identical to the AUTO launch.  (The
-r04 runs of this tool also timed a three-stage load pipeline, since removed: profiles/r04s_h16_depth_sweep_*.)
+of --rounds: tiles per workgroup (RTI_KERNEL_CHUNKS) × 16-pixel groups batched per transposed-read/MFMA round
+(RTI_KERNEL_TILE_DEPTH 1/4/8), each checked bit-identical to the AUTO launch.  (Earlier r04 runs of this tool
+also timed a three-stage load pipeline, since removed: profiles/r04s_h16_depth_sweep_*.)
 
-  python tools/sweep_h16.py --config c3|c4 [--rounds 20] [--tpw 0,8,16]
+  python tools/sweep_h16.py --config c2|c3|c4 [--rounds 20] [--tpw 0,8,16]
 """
 import argparse
 import json
