@@ -1,15 +1,17 @@
 #!/usr/bin/env python3
 """The blocked Cholesky RBF solver (rti_rbf.hip rbf_solve_chol, N > 256) in one process: the solve of a
 400x400 ROI (E = 1 query) with reference-geometry light vectors, median of 5 HIP-event timings, and 64
-sampled pixels of a 100-query evaluation against the fp64 oracle (max |f − f_ref| / max(|f_ref|, 255)).
+sampled pixels of a 100-query evaluation against the fp64 oracle (max |f − f_ref| / max(|f_ref|, 255)), and a
+hash of the whole fp64 evaluation (runs under RTI_RBF_CHOL_LA=0 / 1 must print the same one).
 
   python tools/sweep_chol.py [N ...]"""
+import hashlib
 import json
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "smartphone-based-rti_amd"))
+sys.path.insert(0, os.environ.get("RTI_PKG_DIR", os.path.join(ROOT, "smartphone-based-rti_amd")))  # A/B builds
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -44,5 +46,6 @@ for N in ns:
     out = rti.interpolate_rbf_perpixel(I, lu, lv, q[0], q[1], out_dtype=torch.float64, out_layout="eval")
     got = out.cpu().numpy().reshape(q.shape[1], -1)[:, idx].T
     worst = max(float(np.abs(got[k] - refs[k]).max() / max(np.abs(refs[k]).max(), 255.0)) for k in range(len(idx)))
-    print(json.dumps({"N": N, "solve_ms": round(float(np.median(ms)), 3),
-                      "max_rel_vs_oracle": worst}), flush=True)
+    sha = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(json.dumps({"N": N, "solve_ms": round(float(np.median(ms)), 3), "max_rel_vs_oracle": worst,
+                      "la": os.environ.get("RTI_RBF_CHOL_LA", "1"), "sha": sha}), flush=True)
