@@ -137,16 +137,17 @@ def test_compat_interpolate_and_prepare(cuda):
     assert ok, err
     tables = compat.prepare_images_data(grid)
     ref_t = d["tables"]
-    # int32 truncation can only differ where the reference value sits within 1e-4 of an integer
-    # (fp64 Cholesky normal equations vs the reference's SVD: coefficients agree to ~4e-8
-    # relative).  The flips are counted and reported, not only bounded.
+    # int32 truncation could only differ where the reference value sits within 1e-4 of an integer
+    # (fp64 Cholesky normal equations vs the reference's SVD: coefficients agree to ~4e-8 relative);
+    # 33 of this golden's values do, and none flips — held at zero like the cams path
+    # (test_compat_compute_end_to_end), the kernels being deterministic.
     diff = tables != ref_t
     near = np.abs(np.transpose(d["grid"], (2, 3, 0, 1)) - np.round(np.transpose(d["grid"], (2, 3, 0, 1)))) < 1e-4
     flips = int(diff.sum())
     print(f"per-pixel PTM int32 tables: {flips} of {diff.size} entries differ from the reference "
           f"({int(near.sum())} reference values lie within 1e-4 of an integer)")
-    assert not (diff & ~near).any()
-    assert flips <= int(near.sum()) and flips / diff.size < 1e-4
+    assert int(near.sum()) > 0  # the golden does exercise near-integer truncations
+    assert flips == 0
     assert np.array_equal(compat.prepare_images_data(d["grid"]), ref_t)
     one = compat.interpolate_intensities(data, interpolate_PTM=True, first_only=True)
     assert one.shape == (1, 1, 100, 100)
