@@ -8,9 +8,10 @@
 // pixels and the 2048-pixel tile gives 2-KiB runs per wave and plane with 32-light steps
 // (v_mfma_f32_16x16x32_f16):
 //
-//   * a 512-thread workgroup (one per CU over all channels) streams tiles of 2048 pixels × 32-light steps;
-//     per step wave w loads planes 4w..4w+3 of the tile (two 16-byte non-temporal loads per lane and plane)
-//     into a double-buffered LDS tile [2][32][2048 + 16]; two steps of loads in flight (128 KiB per CU);
+//   * a 512-thread workgroup streams tiles of R pixels × 32-light steps (R = 2048, one workgroup per CU, or
+//     since r04 R = 1024 with two per CU — AUTO for k <= 9); per step wave w loads planes 4w..4w+3 of the tile
+//     (R/1024 16-byte non-temporal loads per lane and plane) into a double-buffered LDS tile [2][32][R + 16];
+//     two steps of loads in flight (128 KiB per CU);
 //   * B operands come back with ds_read_b64_tr_b8 (8 lights of one pixel per lane) and are widened to fp16
 //     exactly: a byte permute makes 1024 + x (0x64xx), a packed fp16 add of −1024 leaves x;
 //   * epilogue: the fp32 sums scaled by 1/s, stored like the q8 form's.
@@ -257,19 +258,32 @@ struct H16Args {
   int want;  // RTI_KERNEL_CHUNKS: tiles per workgroup (0 = AUTO)
   int cb;    // RTI_KERNEL_TILE_DEPTH: batched groups (measurement)
   hipStream_t s;
+  int geom = 0;  // RTI_KERNEL_TILE_WAVES: 0 AUTO, 1 the 2048-pixel tile, 2 the 1024-pixel tile (measurement)
 };
 
 template <int K, int LAYOUT, int R, int STEP>
 int launch_h16_g(const H16Args& a) {
   // one workgroup per CU over all channels, each streaming tpw interleaved tiles
   const int64_t tpc = (a.P + R - 1) / R, cus = device_cus();
-  const int64_t wpc = cus >= a.C ? cus / a.C : 1;
+  const int64_t wpc = (cus >= a.C ? cus / a.C : 1) * (2048 / R);  // workgroups per channel: 2048/R per CU
   const int tpw = a.want ? a.want : (int)((tpc + wpc - 1) / wpc);
   return launch_h16_t<K, LAYOUT, R, STEP>(a.op, a.N, a.I, a.P, a.C, a.ls, a.cs, a.coef, a.ocs, tpw, a.cb, a.s);
 }
 
+// AUTO geometry: 1024-pixel tiles (1-KiB runs per wave and plane, two workgroups per CU) for k <= 9 where two
+// fit in the LDS, else the 2048-pixel tile (one per CU).  Two independent workgroups per CU overlap each other's
+// per-step barrier: c2 u8 0.036 vs 0.0395 ms, c3 u8 0.187 vs 0.193; HSH-16 c4 u8 1.29 either way
+// (profiles/r04h_h16_geometry_sweep_c*.log, bit-identical).
+bool h16_half_tiles(int k, int N, int geom) {
+  if (geom) return geom == 2;
+  return k <= 9 && h16_lds_bytes<1024, 32>(N) <= 80 * 1024;
+}
+
 template <int K>
 int launch_h16_l(int layout, const H16Args& a) {
+  if (h16_half_tiles(K, a.N, a.geom))
+    return layout == RTI_COEF_PLANAR ? launch_h16_g<K, RTI_COEF_PLANAR, 1024, 32>(a)
+                                     : launch_h16_g<K, RTI_COEF_PIXEL_MAJOR, 1024, 32>(a);
   return layout == RTI_COEF_PLANAR ? launch_h16_g<K, RTI_COEF_PLANAR, 2048, 32>(a)
                                    : launch_h16_g<K, RTI_COEF_PIXEL_MAJOR, 2048, 32>(a);
 }
@@ -342,10 +356,11 @@ extern "C" int rti_fit_shared_h16(const void* op, int k, int N, const uint8_t* I
   if (P % 16 || ls % 16 || cs % 16 || !aligned_to(I, 16) || !aligned_to(op, 16) || !aligned_to(coef, 16) || ocs % 4)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_h16: needs P, strides and pointers 16-byte aligned");
   note_launches(1);
-  // RTI_KERNEL_CHUNKS(n): tiles per workgroup = n (measurement)
+  // RTI_KERNEL_CHUNKS(n): tiles per workgroup = n; RTI_KERNEL_TILE_DEPTH(1|4|8): groups batched per round;
+  // RTI_KERNEL_TILE_WAVES(1|2): the 2048- or 1024-pixel tile (measurement)
   const H16Args a{static_cast<const unsigned char*>(op), N, I, P, C, ls, cs, coef, ocs,
                   (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF,
-                  (hipStream_t)stream};
+                  (hipStream_t)stream, (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF};
   switch (k) {
     case 6: return launch_h16_l<6>(coef_layout, a);
     case 9: return launch_h16_l<9>(coef_layout, a);

@@ -85,9 +85,10 @@ def test_auto_is_h16_and_matches_q8(cuda):
 
 
 def test_tile_streams_bit_identical(cuda):
-    """AUTO lets every workgroup stream several interleaved 2048-pixel tiles through one load pipeline; the
-    result equals one cold tile per workgroup (RTI_KERNEL_CHUNKS(1)) and 3 tiles per workgroup bit for bit
-    (ragged P: a partial last tile and a short last stream, 3 channels, HSH-16 and PTM-6)."""
+    """AUTO lets every workgroup stream several interleaved tiles through one load pipeline; the result equals
+    one cold tile per workgroup (RTI_KERNEL_CHUNKS(1)), 3 tiles per workgroup, batched groups and both tile
+    geometries (2048 pixels one workgroup per CU, 1024 pixels two) bit for bit (ragged P: a partial last tile
+    and a short last stream, 3 channels, HSH-16 and PTM-6)."""
     for k, N in ((16, 200), (6, 100)):
         C, P = 3, 2048 * 1050 + 16 * 5
         lu, lv = o.synth_dirs(N, 4)
@@ -96,8 +97,10 @@ def test_tile_streams_bit_identical(cuda):
         g = torch.Generator(device=cuda).manual_seed(5)
         I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda, dtype=torch.uint8)
         outs = []
+        W = L.RTI_KERNEL_TILE_WAVES_SHIFT  # tile geometry: 1 = 2048 pixels, 2 = 1024 pixels (AUTO for k <= 9)
         for flags in (0, 1 << L.RTI_KERNEL_CHUNKS_SHIFT, 3 << L.RTI_KERNEL_CHUNKS_SHIFT,
-                      4 << L.RTI_KERNEL_TILE_DEPTH_SHIFT, 8 << L.RTI_KERNEL_TILE_DEPTH_SHIFT):  # batched groups
+                      4 << L.RTI_KERNEL_TILE_DEPTH_SHIFT, 8 << L.RTI_KERNEL_TILE_DEPTH_SHIFT,  # batched groups
+                      1 << W, 2 << W, (2 << W) | (1 << L.RTI_KERNEL_CHUNKS_SHIFT), (1 << W) | (3 << L.RTI_KERNEL_CHUNKS_SHIFT)):
             coef = torch.full((C, P, k), float("nan"), device=cuda)
             rti.api.fit_h16_into(op, I, coef, k=k, flags=flags)
             outs.append(coef)

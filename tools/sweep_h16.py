@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The 8-bit shared fit (rti_fit_shared_h16) variants interleaved in ONE process, HIP events per launch, median
-of --rounds: tiles per workgroup (RTI_KERNEL_CHUNKS) × 16-pixel groups batched per transposed-read/MFMA round
-(RTI_KERNEL_TILE_DEPTH 1/4/8), each checked bit-identical to the AUTO launch.  (Earlier r04 runs of this tool
+of --rounds: tile geometry (RTI_KERNEL_TILE_WAVES 1/2: 2048 / 1024 pixels) × tiles per workgroup
+(RTI_KERNEL_CHUNKS) × 16-pixel groups batched per transposed-read/MFMA round (RTI_KERNEL_TILE_DEPTH 1/4/8), each
+checked bit-identical to the AUTO launch.  (Earlier r04 runs of this tool
 also timed a three-stage load pipeline, since removed: profiles/r04s_h16_depth_sweep_*.)
 
   python tools/sweep_h16.py --config c2|c3|c4 [--rounds 20] [--tpw 0,8,16]
@@ -39,11 +40,13 @@ def main():
     coef = torch.empty((C, P, k), device=dev)
     ref = torch.empty((C, P, k), device=dev)
     variants = []
-    for tpw in [int(x) for x in args.tpw.split(",")]:
-        for cb in (1, 4, 8):  # groups batched per step (RTI_KERNEL_TILE_DEPTH)
-            fl = (tpw << L.RTI_KERNEL_CHUNKS_SHIFT) | (cb << L.RTI_KERNEL_TILE_DEPTH_SHIFT)
-            variants.append((f"h16_tpw{tpw or 'auto'}_batch{cb}",
-                             lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
+    for half in (1, 2):  # RTI_KERNEL_TILE_WAVES: 1 = 2048-pixel tiles (one workgroup per CU), 2 = 1024 (two)
+        for tpw in [int(x) for x in args.tpw.split(",")]:
+            for cb in (1, 4, 8):  # groups batched per step (RTI_KERNEL_TILE_DEPTH)
+                fl = (tpw << L.RTI_KERNEL_CHUNKS_SHIFT) | (cb << L.RTI_KERNEL_TILE_DEPTH_SHIFT) | \
+                     (half << L.RTI_KERNEL_TILE_WAVES_SHIFT)
+                variants.append((f"h16_{'1024px' if half == 2 else '2048px'}_tpw{tpw or 'auto'}_batch{cb}",
+                                 lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
     rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
     same = {}
     for name, fn in variants:
