@@ -27,37 +27,42 @@ def main():
     ap.add_argument("--basis", default="ptm")
     ap.add_argument("--ns", default="64,96,100,112,128")
     ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--geom", default="0", help="RTI_KERNEL_TILE_WAVES values: 0 AUTO, 1 2048-px, 2 1024-px tiles")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     H, W = (int(x) for x in args.hw.split("x"))
     P, k = H * W, rti.basis_terms(args.basis)
     runs = []
+    geoms = [int(x) for x in args.geom.split(",")]
     for N in [int(x) for x in args.ns.split(",")]:
         lu, lv = bench.synth_dirs(N, 2)
         I8 = bench.synth_stack(H, W, N, 1, args.basis, lu, lv, 1000, dev).clamp(0, 255).to(torch.uint8)
         op = torch.as_tensor(rti.api.h16_operator(rti.pinv(lu, lv, args.basis)), device=dev)
         coef = torch.empty((1, P, k), device=dev)
-        runs.append((N, lambda op=op, I8=I8, coef=coef: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel")))
+        for gm in geoms:
+            fl = gm << rti._lib.RTI_KERNEL_TILE_WAVES_SHIFT
+            runs.append(((N, gm), lambda op=op, I8=I8, coef=coef, fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k,
+                                                                                           layout="pixel", flags=fl)))
     for _, fn in runs:
         fn()
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
-    times = {N: [] for N, _ in runs}
+    times = {key: [] for key, _ in runs}
     for _ in range(args.rounds):
-        for N, fn in runs:
+        for key, fn in runs:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
             fn()
             b.record(stream)
-            times[N].append((a, b))
+            times[key].append((a, b))
         torch.cuda.synchronize()
     res = {}
-    for N, _ in runs:
-        ms = float(np.median([a.elapsed_time(b) for a, b in times[N]]))
+    for (N, gm), _ in runs:
+        ms = float(np.median([a.elapsed_time(b) for a, b in times[(N, gm)]]))
         alg = 1.0 * P * N + 4.0 * P * k
         gbs = alg / (ms * 1e-3) / 1e9
-        res[N] = {"median_ms": ms, "GBps": gbs, "frac_8TBps": gbs / 8000.0, "us_per_light": 1e3 * ms / N}
-        print(f"N={N:4d} {ms:.4f} ms  {gbs:.0f} GB/s ({gbs / 8000:.3f})  {1e3 * ms / N:.3f} us per light",
+        res[f"{N}_g{gm}"] = {"median_ms": ms, "GBps": gbs, "frac_8TBps": gbs / 8000.0, "us_per_light": 1e3 * ms / N}
+        print(f"N={N:4d} geom={gm} {ms:.4f} ms  {gbs:.0f} GB/s ({gbs / 8000:.3f})  {1e3 * ms / N:.3f} us per light",
               flush=True)
     print(json.dumps({"hw": [H, W], "basis": args.basis, "results": res}))
 
