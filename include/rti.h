@@ -198,8 +198,11 @@ int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I, int64_t P,
 /* ---- device: shared fit of 8-bit stacks on the fp16 matrix cores (rti_fit_h16.hip) ----
  * The same contraction as rti_fit_shared_q8 with the operator split as w·s = hi + lo in fp16 (s a power
  * of two per row: 22 significant bits) and fp32 accumulation (v_mfma_f32_16x16x32_f16): the accuracy of
- * the fp32 stream, a quarter of the q8 form's accumulator registers per pixel, so 2048-pixel tiles and
- * 2-KiB runs per wave and plane.  rti_h16_operator builds the operator (rti_h16_operator_bytes(k, N)
+ * the fp32 stream, a quarter of the q8 form's accumulator registers per pixel: 1024-pixel tiles with two
+ * workgroups per CU for k <= 9 (when both fit in the LDS), else 2048-pixel tiles with one; kernel flags
+ * (measurement): RTI_KERNEL_TILE_WAVES(1|2) forces the 2048- / 1024-pixel tile, RTI_KERNEL_CHUNKS(n) n tiles
+ * per workgroup, RTI_KERNEL_TILE_DEPTH(1|4|8) 16-pixel groups per read/MFMA round (all bit-identical).
+ * rti_h16_operator builds the operator (rti_h16_operator_bytes(k, N)
  * bytes, device copy 16-byte aligned) from the fp64 pseudo-inverse (non-finite entries -> RTI_ERR_BAD_ARG).
  * Arguments, alignment and layouts as rti_fit_shared_q8; N <= rti_fit_shared_h16_max_lights().
  * op (here and for rti_fit_shared_q8) must be the operator built for the SAME k and N: the kernel copies
