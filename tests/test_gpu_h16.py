@@ -148,3 +148,25 @@ def test_abi_errors(cuda):
     assert lib.rti_fit_shared_h16(vp(op), 6, 20, vp(I), 48, 1, 48, 0, vp(coef), 0, 0, 0, s) == L.RTI_OK
     with pytest.raises(ValueError):
         rti.h16_operator(np.full((6, 20), np.nan))
+
+
+@pytest.mark.parametrize("basis", ["ptm", "hsh9", "hsh"])
+def test_geometries_at_max_lights(cuda, basis):
+    """At the largest N the LDS takes, the 1024-pixel tile (forced: one workgroup per CU fits there, two do
+    not) and the 2048-pixel tile give the same bits as AUTO, with a partial last tile of each geometry."""
+    Nmax = int(L.lib().rti_fit_shared_h16_max_lights())
+    k = rti.basis_terms(basis)
+    lu, lv = o.synth_dirs(Nmax, 6)
+    pv = np.linalg.pinv(o.design("ptm" if basis == "ptm" else "hsh", lu, lv)[:, :k])  # HSH-9: the first 9 terms
+    op = torch.as_tensor(rti.h16_operator(pv), device=cuda)
+    P = 2048 * 3 + 1024 + 48
+    I = torch.randint(0, 256, (Nmax, P), generator=torch.Generator(device=cuda).manual_seed(7), device=cuda,
+                      dtype=torch.uint8)
+    outs = []
+    for geom in (0, 1, 2):
+        coef = torch.full((1, P, k), float("nan"), device=cuda)
+        rti.api.fit_h16_into(op, I, coef, k=k, flags=geom << L.RTI_KERNEL_TILE_WAVES_SHIFT)
+        outs.append(coef)
+    assert not torch.isnan(outs[0]).any() and all(torch.equal(outs[0], c) for c in outs[1:])
+    err, ok = coef_close(outs[0][0].cpu().numpy(), (pv @ I.double().cpu().numpy()).T)
+    assert ok, err
