@@ -950,36 +950,44 @@ def cpu_baseline(wl, budget_s):
 def cyclic_stack(wl, ctx, chunks):
     """This rank's rows under the block-cyclic partition (rti.parallel.cyclic_rows), generated on the
     device block by block exactly as the block rows are (synth_stack is a function of the global rows),
-    as a light-major [N, h, W] stack of channel 0 in the workload's intensity dtype."""
+    every channel, in the workload's intensity dtype and stack layout: light-major [C, N, h, W] (C = 1:
+    [N, h, W]) or the reference's pixel-major [C, h, W, N] ([h, W, N])."""
     import torch
 
     from rti.parallel import cyclic_rows
 
     blocks = cyclic_rows(ctx.H, ctx.world, ctx.rank, chunks)
-    parts = [synth_stack(ctx.H, wl.W, wl.N, 1, wl.basis, wl.lu, wl.lv, seed=1000, device=ctx.dev, rows=b)[0]
+    parts = [synth_stack(ctx.H, wl.W, wl.N, wl.C, wl.basis, wl.lu, wl.lv, seed=1000, device=ctx.dev, rows=b)
              for b in blocks]
-    I = torch.cat(parts, dim=1).reshape(wl.N, -1, wl.W)
-    return I.to(wl.I.dtype) if I.dtype != wl.I.dtype else I
+    I = torch.cat(parts, dim=2).reshape(wl.C, wl.N, -1, wl.W)
+    del parts
+    if I.dtype != wl.I.dtype:
+        I = I.to(wl.I.dtype)
+    if wl.stack == "pixel":
+        I = I.permute(0, 2, 3, 1).contiguous()
+    return I if wl.C > 1 else I[0]
 
 
 def e2e_parity(wl, ctx, full, chunks, per_block=256):
-    """Rank 0: sampled pixels of EVERY row block of the gathered [H, W, k] map (all ranks' blocks, block-
-    cyclic order) against the oracle on that block's regenerated intensities — checks the fit and that
-    every block landed in its place."""
+    """Rank 0: sampled pixels of EVERY row block of the gathered map (all ranks' blocks, block-cyclic
+    order; channels 0 and C - 1) against the oracle on that block's regenerated intensities — checks the
+    fit and that every block landed in its place."""
     from rti.parallel import cyclic_rows
 
     o = oracle()
     worst, checked = 0.0, 0
+    fullc = full if wl.C > 1 else full.unsqueeze(0)
     for r in range(ctx.world):
         for bi, (r0, r1) in enumerate(cyclic_rows(ctx.H, ctx.world, r, chunks)):
-            I = synth_stack(ctx.H, wl.W, wl.N, 1, wl.basis, wl.lu, wl.lv, seed=1000, device=ctx.dev, rows=(r0, r1))[0]
+            I = synth_stack(ctx.H, wl.W, wl.N, wl.C, wl.basis, wl.lu, wl.lv, seed=1000, device=ctx.dev, rows=(r0, r1))
             if wl.in_bytes == 1:
                 I = I.to(wl.I.dtype)
             idx = sample_idx((r1 - r0) * wl.W, per_block, 17 + 31 * r + bi)
-            ref = o.fit_shared(I[:, idx].float().cpu().numpy(), wl.pinv64)
-            got = full[r0:r1].reshape(-1, wl.k)[idx].cpu().numpy()
-            worst = max(worst, coef_parity(got, ref))
-            checked += len(idx)
+            for c in sorted({0, wl.C - 1}):
+                ref = o.fit_shared(I[c][:, idx].float().cpu().numpy(), wl.pinv64)
+                got = fullc[c][r0:r1].reshape(-1, wl.k)[idx].cpu().numpy()
+                worst = max(worst, coef_parity(got, ref))
+                checked += len(idx)
     return {"max_rel": worst, "tol": 1e-4, "ok": bool(worst <= 1e-4), "checked_px": checked,
             "blocks": ctx.world * chunks, "vs": "oracle fit_shared on each block's regenerated rows"}
 
@@ -995,15 +1003,19 @@ def allgather_legs(wl, ctx, reps=5):
     from rti.parallel import RowTiledFitter, gather_rows
 
     dev = ctx.dev
-    local = wl.coef[0].reshape(ctx.h, wl.W, wl.k) if wl.args.layout == "pixel" else \
-        wl.coef[0].T.reshape(ctx.h, wl.W, wl.k).contiguous()
+    locals_ = [(wl.coef[c].reshape(ctx.h, wl.W, wl.k) if wl.args.layout == "pixel" else
+                wl.coef[c].T.reshape(ctx.h, wl.W, wl.k).contiguous()) for c in range(wl.C)]
+
+    def gather_all():  # every channel's rows (one collective per channel)
+        for loc in locals_:
+            gather_rows(loc, ctx.H)
     for _ in range(2):
-        gather_rows(local, ctx.H)
+        gather_all()
     torch.cuda.synchronize(dev)
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        gather_rows(local, ctx.H)
+        gather_all()
     torch.cuda.synchronize(dev)
     gather_ms = (time.perf_counter() - t0) / reps * 1e3
     # cyclic blocks of H/(G*chunks) rows (4K on 8 GPUs: 2160/8 = 270 rows per rank -> 3 chunks of 90)
@@ -1011,7 +1023,10 @@ def allgather_legs(wl, ctx, reps=5):
         return gather_ms, None, 0, {"skipped": f"H={ctx.H} is not a multiple of {ctx.world} ranks", "ok": True}
     chunks = next((c for c in (4, 3, 2, 1) if ctx.H % (ctx.world * c) == 0), 1)
     I_cyc = cyclic_stack(wl, ctx, chunks)
-    fitter = RowTiledFitter(I_cyc, wl.lu, wl.lv, ctx.H, basis=wl.basis, chunks=chunks, partition="cyclic")
+    # the same kernel family as the 1-GPU line: every channel, the stack's layout (rti_fit_shared_pm for the
+    # reference's pixel-major stacks), 8-bit stacks on the h16 matrix-core fit
+    fitter = RowTiledFitter(I_cyc, wl.lu, wl.lv, ctx.H, basis=wl.basis, chunks=chunks, partition="cyclic",
+                            stack=wl.stack, kernel=wl.args.kernel)
     for _ in range(2):
         fitter()
     torch.cuda.synchronize(dev)

@@ -1321,6 +1321,11 @@ using namespace rti;
 extern "C" int rti_fit_shared(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
                               int64_t light_stride, int64_t channel_stride, float* coef, int coef_layout,
                               int64_t coef_channel_stride, int kernel, rti_stream_t stream) {
+  constexpr int flags = RTI_KERNEL_NONTEMPORAL | RTI_KERNEL_PINV_LDS | RTI_KERNEL_NT_STORE | RTI_KERNEL_STAGE |
+                        RTI_KERNEL_ROTATE | RTI_KERNEL_ROUNDS | RTI_KERNEL_ONE_LAUNCH | RTI_FIELD_CHUNKS |
+                        RTI_FIELD_TILE_PLANES | RTI_FIELD_TILE_DEPTH | RTI_FIELD_TILE_WAVES;
+  if (!kernel_bits_ok(kernel, RTI_KERNEL_TILE, flags))
+    return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: unknown kernel bits 0x%x", kernel);
   if (!pinv || !I || !coef) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: null pointer");
   if (N <= 0 || P <= 0 || C <= 0 || C > 65535) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: bad N/P/C");
   if (k < 1 || k > 16) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared: k=%d outside 1..16", k);

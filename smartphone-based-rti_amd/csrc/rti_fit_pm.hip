@@ -39,10 +39,17 @@ typedef int intx2 __attribute__((ext_vector_type(2)));
 
 constexpr int PM_LDS = 160 * 1024;
 constexpr uint32_t PM_OOB = 0x80000000u;  // buffer offset past every num_records: the store is dropped
-constexpr uint32_t PM_OOB_ALL = 0xFFFFFFF0u;  // the same for a buffer over the whole coefficient array (< 2^32 - 16 B)
 
-__device__ __forceinline__ void dma16(const void* g, float* lds) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 2 /* nt */);
+// One 1-KiB LDS-DMA (buffer_load_dwordx4 … lds): lane l's 16 bytes at src + voff + soff go to lds + 16·l.
+// The descriptor bounds every read (a lane past num_records gets zeros), so no DMA can leave its run.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t src, int voff, int soff, void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0,
+                                           2 /* nt */);
+}
+
+// a descriptor over `bytes` bytes at p (bytes < 2^32)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(uint32_t)bytes, 0x00020000);
 }
 
 template <typename T>
@@ -143,11 +150,11 @@ fit_pm_dma(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64
   const int L = (int)((bbytes + 1023) >> 10);  // DMA instructions per block
   auto issue = [&](int64_t u, int s) {
     const int64_t c = u / nblk, b = u - c * nblk;
-    const char* base = reinterpret_cast<const char*>(I + c * cstride);
-    int64_t off = b * bbytes + 16 * lane;
+    const int64_t rest = cbytes - b * bbytes;  // the block, or the channel's partial last block
+    const __amdgpu_buffer_rsrc_t src =
+        rsrc_at(reinterpret_cast<const char*>(I + c * cstride) + b * bbytes, rest < bbytes ? rest : bbytes);
     float* dst = ring + s * slot;
-    for (int i = 0; i < L; ++i, off += 1024)  // lanes past the channel re-read its last 16 B (never used)
-      dma16(base + (off + 16 <= cbytes ? off : cbytes - 16), dst + i * 256);
+    for (int i = 0; i < L; ++i) dma16(src, 16 * lane, i << 10, dst + i * 256);  // lanes past the block read zeros
   };
   const int q = lane & 15, r = lane >> 4;
   const int nfull = N >> 4;  // whole 16-light chunks; a partial last chunk is masked
@@ -284,24 +291,23 @@ fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
   const int ng = (int)(nk * U);                 // groups of the stream
   const int dt = (int)(nk * ((U * GBY) >> 10));  // DMAs of the stream
   const int ust = (int)ustep;
-  // DMA cursor: unit ud of channel cd, `left` DMAs of it still to issue, the lane's 64-bit source pointer
-  // gp (advanced by 1 KiB per DMA, rebuilt at unit changes) and the lane's last readable address gend (the
-  // channel's last 16 B: lanes past the channel re-read them, unused), ring byte wslot
+  // DMA cursor: unit ud of channel cd, `left` DMAs of it still to issue, the unit's descriptor src (bounded by
+  // the unit, or by the channel's end for its partial last unit) and the byte inb inside the unit; ring byte wslot
   int cd = (int)(u0 / nu), ud = (int)(u0 - (int64_t)cd * nu);
   int cg = cd, ug = ud;  // group cursor (below): unit ug of channel cg, group gi within the unit
   const int UB = U * GBY, UKB = UB >> 10;
-  const char* gp;
-  const char* gend;
+  __amdgpu_buffer_rsrc_t src;
+  int inb = 0;
   auto seek = [&]() {
-    const char* ch = reinterpret_cast<const char*>(I + cd * cstride);
-    gp = ch + (int64_t)ud * UB + 16 * lane;
-    gend = ch + cbytes - 16;
+    const int64_t ub = (int64_t)ud * UB, rest = cbytes - ub;
+    src = rsrc_at(reinterpret_cast<const char*>(I + cd * cstride) + ub, rest < UB ? rest : UB);
+    inb = 0;
   };
   seek();
   int left = UKB, wslot = 0;
   auto issue = [&]() {
-    dma16(gp < gend ? gp : gend, reinterpret_cast<float*>(rp + wslot));
-    gp += 1024;
+    dma16(src, 16 * lane, inb, rp + wslot);
+    inb += 1024;
     wslot += 1024;
     wslot = wslot == ring ? 0 : wslot;
     if (--left == 0) {  // next unit (no division: ustep = GW or 1 is far below nu in practice)
@@ -402,27 +408,30 @@ fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
   }
 }
 
-// VALU streaming form (AUTO for k <= 9): the same units, interleaving and LDS ring as fit_pm_stream, but the
-// ring is consumed 64 pixels (4 groups of the stream) at a time with ONE PIXEL PER LANE: lane l reads its
-// pixel's row from the ring (ds_read_b128, 4 lights) and accumulates k coefficients with packed FMAs
-// (v_pk_fma_f32 over light pairs: acc_i.xy += I[n, n+1]·pinv[i][n, n+1], the weights wave-uniform in SGPRs,
-// read by scalar loads), so a pixel·light costs k/2 VALU lane-ops instead of the 16 MACs a 16x16x4 MFMA
-// spends on it whatever k (PTM-6: 10 of 16 matrix rows idle).  The lanes of a block may belong to different
-// units and channels: each lane keeps its own group cursor, and the coefficients leave by buffer stores
-// over the WHOLE coefficient array (per-lane 32-bit offsets; lanes past P or past the stream get an
-// out-of-range offset), so every block issues the same SB stores.
-// MODE (measurement, rti_fit_shared_pm flags): 0 = the fit; 1 = no coefficient stores (RTI_KERNEL_ONE_LAUNCH);
-// 2 = no arithmetic, the stream waited for and zeros stored (RTI_KERNEL_ROUNDS); 3 = the weights of the 4-light
-// steps by wave-uniform scalar loads into SGPRs (RTI_KERNEL_PINV_LDS's opposite, a measurement variant) instead
-// of broadcast ds_read_b128 from the LDS copy: 0.667 against 0.633 ms on c3 (profiles/r04s_pm_sweep_c3.log) —
-// the scalar loads return out of order, so each half step waits on lgkmcnt(0)
-template <int K, typename T, int LAYOUT, int ALIGN, int MODE = 0>
-__global__ void __launch_bounds__(512)
-fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
-               float* __restrict__ coef, int64_t ocstride, int C, int U, int nu, int64_t tu, int ring,
-               uint32_t coef_bytes) {
+// VALU form (AUTO for k <= 9), r05: LAUNCH GENERATIONS with the coefficients parked in registers.
+// A launch covers a range of one channel's 64-pixel blocks; wave w of its GW waves owns ONE contiguous run
+// of nb <= MB blocks (nb·64·N values) and streams it HBM -> a private LDS ring of `ring` bytes with 1-KiB
+// LDS-DMAs (buffer_load_dwordx4 … lds: the descriptor covers exactly the run, so a lane past it reads
+// zeros and no DMA can leave the stack), keeping the ring full.  Lane l computes pixel l of each block
+// (its row read from the ring by ds_read_b128, k coefficients by packed FMAs over light pairs, the
+// weights broadcast from an LDS copy) and PARKS the k coefficients of block j in registers
+// park[j][0..k-1] (j is a compile-time index: the block loop is unrolled MB times around the rolled
+// light loop).  Only after its last block does the wave store, so every wave of the chip reads during
+// the launch and writes at its end: the read/write phase separation the light-major fit gets from its
+// own launch generations (the r04 form stored every block as it finished, "spread"
+// through the read stream, and lost 0.13 ms of 0.63 on c3 to that placement).
+// Waits: before block j the wave needs the DMA holding the block's last byte; only DMAs are in flight
+// (no stores until the end), so vmcnt = the DMAs issued after it, exactly.
+// IL = 1: the launch's UNITS (U blocks, U = 4 / gcd(N, 4): whole KiB of 4-byte values) are dealt to the waves
+// round-robin (wave w: units w, w + GW, …), so at any moment the chip reads one contiguous slab of the stack,
+// as the light-major fit's waves do; IL = 0: each wave one contiguous run of blocks.  The two are
+// bit-identical; the wave's run is then a list of unit segments, each with its own bounded descriptor.
+// PROBE (not reachable from the C ABI; tools/probe/pm_probe.hip): 1 = no coefficient stores.
+template <int K, typename T, int LAYOUT, int ALIGN, int MB, int IL = 1, int PROBE = 0>
+__global__ void __launch_bounds__(384)
+fit_pm_vgen(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, float* __restrict__ coef,
+            int64_t pb, int64_t nblk, int ring, int ulog) {
   typedef float f2 __attribute__((ext_vector_type(2)));
-  constexpr int SB = MODE == 1 ? 0 : (LAYOUT == RTI_COEF_PIXEL_MAJOR ? (K % 2 == 0 ? K / 2 : K) : K);  // stores per block
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int W = blockDim.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -437,176 +446,156 @@ fit_pm_vstream(const float* __restrict__ pinv, int N, const T* __restrict__ I, i
   __syncthreads();
   char* __restrict__ rp = reinterpret_cast<char*>(lds + N4 * K) + wave * ring;
   const int64_t gw = (int64_t)blockIdx.x * W + wave, GW = (int64_t)gridDim.x * W;
-  const int GBY = 16 * N * (int)sizeof(T);
-  const int64_t cbytes = P * N * (int64_t)sizeof(T);
-  const int slots = ring >> 10;
-  const int64_t nk = gw >= tu ? 0 : (tu - 1 - gw) / GW + 1;  // units w, w + GW, ...
-  if (nk == 0) return;
-  const int ust = (int)GW;
-  const int ng = (int)(nk * U);                  // groups of the stream
-  const int nb = (ng + 3) >> 2;                   // 64-pixel blocks
-  const int dt = (int)(nk * ((U * GBY) >> 10));  // DMAs of the stream
-  int cd = (int)(gw / nu), ud = (int)(gw - (int64_t)cd * nu);
-  const int UB = U * GBY, UKB = UB >> 10;
-  const char* gp;
-  const char* gend;
-  auto seek = [&]() {
-    const char* ch = reinterpret_cast<const char*>(I + cd * cstride);
-    gp = ch + (int64_t)ud * UB + 16 * lane;
-    gend = ch + cbytes - 16;
+  const int RB = N * (int)sizeof(T);  // bytes of one pixel row
+  const int BB = 64 * RB;             // bytes of one block
+  // this wave's blocks of the launch (IL: units of U = 2^ulog blocks; the launch covers nblk blocks = whole
+  // units from block pb/64 on, except at the channel's end)
+  int64_t px0, pxe;  // IL = 0: pixels [px0, pxe)
+  int nb, bytes, cnt = 1;
+  const int U = 1 << ulog, UB = BB << ulog;
+  const int64_t u0 = pb / (64 * U) + gw;  // IL: this wave's first unit (units u0, u0 + GW, …)
+  if constexpr (IL) {
+    const int64_t nun = (nblk + U - 1) >> ulog;
+    if (gw >= nun) return;
+    cnt = (int)((nun - 1 - gw) / GW + 1);
+    const int64_t last = (u0 + (int64_t)(cnt - 1) * GW) * U * 64;  // first pixel of the last unit
+    const int lastpx = (int)(P - last < 64 * U ? P - last : 64 * U);
+    nb = ((cnt - 1) << ulog) + (lastpx + 63) / 64;
+    bytes = (cnt - 1) * UB + lastpx * RB;
+    px0 = pxe = 0;
+  } else {
+    const int64_t b0 = nblk * gw / GW, b1 = nblk * (gw + 1) / GW;
+    nb = (int)(b1 - b0);
+    if (nb <= 0) return;
+    px0 = pb + 64 * b0;
+    pxe = pb + 64 * b1 < P ? pb + 64 * b1 : P;
+    bytes = (int)(pxe - px0) * RB;
+  }
+  // descriptors: IL = unit s of the wave (UB bytes, or the channel's partial last unit), else the whole run;
+  // num_records rounded up to 16 B so a segment's last 16-B DMA piece is in range (a segment starts 256-B
+  // aligned; one that ends before P is followed by the channel's next pixels, one that ends at P by the
+  // channel's 16-B aligned end: pm_dma_shape, P·N % 4 == 0, I 16-byte aligned)
+  auto seg_src = [&](int sg) {
+    if constexpr (IL) {
+      const int64_t p0 = (u0 + sg * GW) * U * 64;
+      const int64_t rest = (P - p0) * RB;
+      return rsrc_at(I + p0 * N, ((rest < UB ? rest : UB) + 15) & ~15);
+    } else {
+      return rsrc_at(I + px0 * N, (bytes + 15) & ~15);
+    }
   };
-  seek();
-  int left = UKB, wslot = 0;
+  const int seg_kb = IL ? UB >> 10 : 0x7fffffff;  // DMAs per segment
+  const int dt = (bytes + 1023) >> 10;            // DMAs of the run
+  const int slots = ring >> 10;
+  int issued = 0, wslot = 0, seg = 0, dseg = 0;
+  __amdgpu_buffer_rsrc_t src = seg_src(0);
   auto issue = [&]() {
-    dma16(gp < gend ? gp : gend, reinterpret_cast<float*>(rp + wslot));
-    gp += 1024;
+    dma16(src, 16 * lane, dseg << 10, rp + wslot);
     wslot += 1024;
     wslot = wslot == ring ? 0 : wslot;
-    if (--left == 0) {
-      left = UKB;
-      ud += ust;
-      while (ud >= nu) {
-        ud -= nu;
-        ++cd;
-      }
-      if (cd < C) seek();
+    if (++dseg == seg_kb) {
+      dseg = 0;
+      if (++seg < cnt) src = seg_src(seg);
     }
   };
-  int issued = dt < slots ? dt : slots;
-  for (int d = 0; d < issued; ++d) issue();
-  // the lane's group cursor: stream group j = 4b + (lane >> 4) -> unit (lc, lu), group gi within it
-  int lc = (int)(gw / nu), lu = (int)(gw - (int64_t)lc * nu), gi = lane >> 4;  // (the prologue moved cd, ud)
-  {
-    while (gi >= U) {
-      gi -= U;
-      lu += ust;
-      while (lu >= nu) {
-        lu -= nu;
-        ++lc;
+  for (const int pro = dt < slots ? dt : slots; issued < pro; ++issued) issue();
+  float park[MB][K];
+  int base = 0;  // ring byte of block j's first byte
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    if (j < nb) {
+      const int end = BB * (j + 1) < bytes ? BB * (j + 1) : bytes;  // (bytes: the run's last byte + 1)
+      wait_vm_dyn(issued - ((end + 1023) >> 10));  // the DMAs issued after the one holding the block's last byte
+      int a0 = base + RB * lane;
+      a0 -= a0 >= ring ? ring : 0;
+      f2 acc[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) acc[i] = f2{0.f, 0.f};
+      float acc1[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) acc1[i] = 0.f;
+      int n = 0;
+      if constexpr (ALIGN == 4) {
+        // one step of 4 lights ahead: step n + 4's row values and weights are read while step n's 2·K
+        // packed FMAs issue (ping-pong register sets, no loop-carried copies)
+        auto rdx = [&](int nn) {
+          int a = a0 + nn * (int)sizeof(T);
+          a -= a >= ring ? ring : 0;
+          return lds4<4, T>(reinterpret_cast<const float*>(rp + a), 0);
+        };
+        auto wts = [&](int nn, int i) { return *reinterpret_cast<const floatx4*>(lw + nn * K + 4 * i); };
+        auto step = [&](const floatx4& x, const floatx4 (&w)[K]) {
+          const f2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]};
+#pragma unroll
+          for (int i = 0; i < K; ++i) {
+            acc[i] = x01 * f2{w[i][0], w[i][1]} + acc[i];
+            acc[i] = x23 * f2{w[i][2], w[i][3]} + acc[i];
+          }
+        };
+        const int n4 = N & ~3;
+        if (n4 > 0) {
+          floatx4 xa = rdx(0), xb, wa[K], wb[K];
+#pragma unroll
+          for (int i = 0; i < K; ++i) wa[i] = wts(0, i);
+          for (n = 0; n < n4; n += 8) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this half's operands
+            if (n + 4 < n4) {
+              xb = rdx(n + 4);
+#pragma unroll
+              for (int i = 0; i < K; ++i) wb[i] = wts(n + 4, i);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            step(xa, wa);
+            if (n + 4 >= n4) break;
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            if (n + 8 < n4) {
+              xa = rdx(n + 8);
+#pragma unroll
+              for (int i = 0; i < K; ++i) wa[i] = wts(n + 8, i);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            step(xb, wb);
+          }
+          n = n4;
+        }
       }
+      for (; n < N; ++n) {  // N % 4 (or every light when the rows are not 16-byte aligned)
+        int a = a0 + n * (int)sizeof(T);
+        a -= a >= ring ? ring : 0;
+        const float x = to_f(*reinterpret_cast<const T*>(rp + a));
+#pragma unroll
+        for (int i = 0; i < K; ++i) acc1[i] = fmaf(x, lw[(n >> 2) * 4 * K + 4 * i + (n & 3)], acc1[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < K; ++i) park[j][i] = (acc[i][0] + acc[i][1]) + acc1[i];
+      // refill every KiB the blocks 0..j freed
+      const int lim0 = (BB * (j + 1) + ring) >> 10;
+      for (const int lim = lim0 < dt ? lim0 : dt; issued < lim; ++issued) issue();
+      base += BB;  // (BB < ring)
+      base -= base >= ring ? ring : 0;
     }
   }
-  const int q = lane & 15;
-  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef, (short)0, (int)coef_bytes, 0x00020000);
-  int base = 0, gd = -1;
-  const int lrow = N * (int)sizeof(T) * lane;  // the lane's row inside a block
-  for (int b = 0; b < nb; ++b) {
-    const int gend_b = 4 * (b + 1) < ng ? 4 * (b + 1) : ng;
-    const int end = GBY * gend_b;
-    const int dn = ((end + 1023) >> 10) - 1;
-    // the refill after block g issues DMAs up to (GBY·min(4(g+1), ng) + ring)/1 KiB (prologue: ring/1 KiB)
-    while (((GBY * (4 * (gd + 1) < ng ? 4 * (gd + 1) : ng) + ring) >> 10) < dn + 1) ++gd;
-    const int nwait = (issued - 1 - dn) + SB * (b - 1 - gd);
-    wait_vm_dyn(nwait > 63 ? 63 : nwait);
-    int a0 = base + lrow;
-    a0 -= a0 >= ring ? ring : 0;
-    f2 acc[K];
+  if constexpr (PROBE == 1) {  // measurement (tools/probe): keep the arithmetic, drop the stores
+    float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < K; ++i) acc[i] = f2{0.f, 0.f};
-    float acc1[K];
+    for (int j = 0; j < MB; ++j)
 #pragma unroll
-    for (int i = 0; i < K; ++i) acc1[i] = 0.f;
-    int n = MODE == 2 ? N : 0;
-    if constexpr (ALIGN == 4 && MODE != 2) {
-      // one step of 4 lights ahead: step n + 4's row values and weights are read (LDS: in order, counted
-      // waits) while step n's 2·K packed FMAs issue
-      auto rdx = [&](int nn) {
-        int a = a0 + nn * (int)sizeof(T);
-        a -= a >= ring ? ring : 0;
-        return lds4<4, T>(reinterpret_cast<const float*>(rp + a), 0);
-      };
-      auto step = [&](const floatx4& x, const floatx4 (&w)[K]) {
-        const f2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]};
+      for (int i = 0; i < K; ++i) t += park[j][i];
+    if (t == -1.2345f) coef[0] = t;
+    return;
+  }
+  // the burst: every parked coefficient, block by block (lanes past the run store nothing)
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-          acc[i] = x01 * f2{w[i][0], w[i][1]} + acc[i];
-          acc[i] = x23 * f2{w[i][2], w[i][3]} + acc[i];
-        }
-      };
-      const int n4 = N & ~3;
-      if (n4 > 0) {
-        // weights pinv[i][n .. n+3]: broadcast reads of the LDS copy, or scalar loads into SGPRs (MODE 3)
-        auto wts = [&](int nn, int i) {
-          return MODE == 3 ? *reinterpret_cast<const floatx4*>(pinv + i * N + nn)
-                           : *reinterpret_cast<const floatx4*>(lw + nn * K + 4 * i);
-        };
-        // ping-pong register sets (no loop-carried copies): each half issues the next step's loads, then the
-        // FMAs of the step loaded one half earlier (scalar loads return out of order, so the only wait, at the
-        // top of a half, is lgkmcnt(0) on the loads issued a whole FMA block before)
-        floatx4 xa = rdx(0), xb, wa[K], wb[K];
+  for (int j = 0; j < MB; ++j) {
+    const int64_t px = IL ? ((u0 + (int64_t)(j >> ulog) * GW) * U + (j & (U - 1))) * 64 + lane : px0 + 64 * j + lane;
+    if (j < nb && px < (IL ? P : pxe)) {
+      if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0) {
 #pragma unroll
-        for (int i = 0; i < K; ++i) wa[i] = wts(0, i);
-        for (n = 0; n < n4; n += 8) {
-          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this half's operands, before the next loads go out
-          if (n + 4 < n4) {
-            xb = rdx(n + 4);
+        for (int i = 0; i < K; i += 2)
+          *reinterpret_cast<f2*>(coef + px * K + i) = f2{park[j][i], park[j][i + 1]};
+      } else {
 #pragma unroll
-            for (int i = 0; i < K; ++i) wb[i] = wts(n + 4, i);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          step(xa, wa);
-          if (n + 4 >= n4) break;
-          __builtin_amdgcn_s_waitcnt(0xC07F);
-          if (n + 8 < n4) {
-            xa = rdx(n + 8);
-#pragma unroll
-            for (int i = 0; i < K; ++i) wa[i] = wts(n + 8, i);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          step(xb, wb);
-        }
-        n = n4;
-      }
-    }
-    for (; n < N; ++n) {  // N % 4 (or every light when the rows are not 16-byte aligned)
-      int a = a0 + n * (int)sizeof(T);
-      a -= a >= ring ? ring : 0;
-      const float x = to_f(*reinterpret_cast<const T*>(rp + a));
-#pragma unroll
-      for (int i = 0; i < K; ++i) acc1[i] = fmaf(x, lw[(n >> 2) * 4 * K + 4 * i + (n & 3)], acc1[i]);
-    }
-    float c[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) c[i] = (acc[i][0] + acc[i][1]) + acc1[i];
-    if constexpr (MODE == 1) {  // measurement: keep the arithmetic, drop the stores
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < K; ++i) t += c[i];
-      if (t == -1.2345f) coef[0] = t;  // never taken for the bench's data (a plain store, not counted by SB)
-    } else
-    {
-    // stores: pixel px of channel lc; lanes past the stream or past P drop theirs
-    const int px = (lu * U + gi) * 16 + q;
-    const bool ok = 4 * b + (lane >> 4) < ng && px < P;
-    const uint32_t cb = (uint32_t)((int64_t)lc * ocstride * 4);
-    if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0) {
-#pragma unroll
-      for (int i = 0; i < K; i += 2) {
-        const uint32_t off = ok ? cb + (uint32_t)((px * K + i) * 4) : PM_OOB_ALL;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(intx2, f2{c[i], c[i + 1]}), rs, off, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        const int64_t e = LAYOUT == RTI_COEF_PIXEL_MAJOR ? (int64_t)px * K + i : (int64_t)i * P + px;
-        const uint32_t off = ok ? cb + (uint32_t)(e * 4) : PM_OOB_ALL;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(c[i]), rs, off, 0, 0);
-      }
-    }
-    }
-    // refill every KiB the blocks 0..b freed
-    const int lim0 = (end + ring) >> 10;
-    const int lim = lim0 < dt ? lim0 : dt;
-    for (; issued < lim; ++issued) issue();
-    base += 4 * GBY;
-    base -= base >= ring ? ring : 0;
-    gi += 4;  // the lane's next group: 4 further along the stream
-    while (gi >= U) {
-      gi -= U;
-      lu += ust;
-      while (lu >= nu) {
-        lu -= nu;
-        ++lc;
+        for (int i = 0; i < K; ++i) coef[LAYOUT == RTI_COEF_PIXEL_MAJOR ? px * K + i : (int64_t)i * P + px] = park[j][i];
       }
     }
   }
@@ -786,7 +775,6 @@ struct PmArgs {
   int layout;
   int64_t ocs;
   hipStream_t stream;
-  int mode = 0;  // measurement variants of the VALU stream (fit_pm_vstream MODE)
 };
 
 // LDS plan of the DMA kernel: G groups of 16 pixels per block, W waves per workgroup
@@ -940,23 +928,20 @@ int launch_stream(const PmArgs& a, const StreamPlan& pl) {
   }
 }
 
-// VALU stream (k <= 9): one workgroup of W waves per CU (W <= 6), a ring per wave that holds a 64-pixel block
-// (4 groups) + 1 KiB; AUTO takes the most waves that fit (6 up to N = 100 for 4-byte values, 4 up to 150).
-// Measured and not kept (profiles/r04w-r04y_pm_sweep_c3*.log, c3 against 0.627–0.635 ms for this form): two
-// lanes per pixel at 8 waves 0.628–0.631, the coefficients of 4–8 blocks held in registers and stored as
-// one burst 0.649–0.657, launch generations with the coefficients staged in LDS and written at each
-// launch's end 0.91–1.01 (the minimum rings starve the stream).  Without its stores this form runs 0.50 ms
-// (RTI_KERNEL_ONE_LAUNCH): the reads and arithmetic are at the light-major fit's speed, the spread stores are
-// what costs.
+// VALU generations (k <= 9): one workgroup of W waves per CU (W <= 6), a ring per wave that holds a block
+// (64 pixel rows) + 1 KiB; AUTO takes the most waves that fit (6 up to N = 100 for 4-byte values, 4 up to
+// 150).  MB (blocks a wave parks per launch: MB·k VGPRs) = 24 for k = 6, 12 for k = 9; a channel's blocks
+// are cut into the fewest launches whose waves park at most MB blocks each, split evenly (c3 4K×100: 4
+// launches of 32 400 blocks, 21–22 per wave).
 struct VPlan {
   int W = 0, ring = 0;
   size_t lds = 0;
 };
 
-VPlan vstream_plan(int k, int N, size_t es, int w_req) {
-  if (k > 9) return VPlan();
-  const int64_t need = (int64_t)4 * 16 * N * es + 1024;
-  const size_t op = (size_t)((N + 3) & ~3) * (k <= 6 ? 6 : 9) * sizeof(float);
+VPlan vgen_plan(int k, int N, size_t es, int w_req) {
+  if (k != 6 && k != 9) return VPlan();
+  const int64_t need = (int64_t)64 * N * es + 1024;
+  const size_t op = (size_t)((N + 3) & ~3) * k * sizeof(float);
   for (int W : {6, 5, 4, 3, 2, 1}) {
     if (w_req && W != w_req) continue;
     const int ring = (int)(((PM_LDS - op) / W) >> 10 << 10);
@@ -970,45 +955,69 @@ VPlan vstream_plan(int k, int N, size_t es, int w_req) {
   return VPlan();
 }
 
+constexpr int vgen_mb(int k) { return k <= 6 ? 24 : 12; }
+
+// launches of one channel, in units of U = 2^ulog blocks: every wave parks at most MB blocks (MB / U units)
+struct VGens {
+  int64_t nbc = 0, per = 0;  // blocks of the channel, blocks per launch (a multiple of U; the last takes the rest)
+  int launches = 0;
+};
+
+VGens vgen_split(int64_t P, int k, int64_t GW, int g_req, int ulog) {
+  VGens g;
+  g.nbc = (P + 63) / 64;
+  const int64_t nun = (g.nbc + (1 << ulog) - 1) >> ulog, cap = GW * (vgen_mb(k) >> ulog);
+  int64_t L = (nun + cap - 1) / cap;
+  if (g_req > L) L = g_req;  // more (smaller) generations: measurement
+  g.per = ((nun + L - 1) / L) << ulog;
+  g.launches = (int)((g.nbc + g.per - 1) / g.per);
+  return g;
+}
+
+// units of whole KiB: U = 4 / gcd(N, 4) 64-pixel blocks of 4-byte values
+inline int vgen_ulog(int N) { return N % 4 == 0 ? 0 : N % 2 == 0 ? 1 : 2; }
+
 template <int K, typename T, int LAYOUT, int ALIGN>
-int launch_vstream_t(const PmArgs& a, const VPlan& pl) {
-  auto kern = a.mode == 1   ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 1>
-              : a.mode == 2 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 2>
-              : a.mode == 3 ? fit_pm_vstream<K, T, LAYOUT, ALIGN, 3>
-                            : fit_pm_vstream<K, T, LAYOUT, ALIGN, 0>;
+int launch_vgen_t(const PmArgs& a, const VPlan& pl, int g_req, bool contig) {
+  constexpr int MB = vgen_mb(K);
+  auto kern = contig ? fit_pm_vgen<K, T, LAYOUT, ALIGN, MB, 0> : fit_pm_vgen<K, T, LAYOUT, ALIGN, MB, 1>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)pl.lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
   const int64_t cus = device_cus();
-  int g = 16, nn = a.N;  // U = 16 / gcd(N, 16): units of a whole number of KiB
-  while (g > 1 && nn % g) g >>= 1;
-  const int U = 16 / g;
-  const int64_t nu = (a.P + 16 * U - 1) / (16 * U), tu = nu * a.C;
-  if (nu >= ((int64_t)1 << 31) / (16 * U)) return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: P too large");
-  const int64_t wgs = (tu + pl.W - 1) / pl.W;
-  const unsigned grid = (unsigned)(wgs < cus ? wgs : cus);
-  const uint64_t cb = (uint64_t)a.ocs * (a.C - 1) * 4 + (uint64_t)a.P * K * 4;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * pl.W), pl.lds, a.stream, a.pinv, a.N, static_cast<const T*>(a.I),
-                     a.P, a.cs, a.coef, a.ocs, a.C, U, (int)nu, tu, pl.ring, (uint32_t)cb);
+  const int ulog = contig ? 0 : vgen_ulog(a.N);
+  const VGens g = vgen_split(a.P, K, cus * pl.W, g_req, ulog);
+  int launches = 0;
+  for (int c = 0; c < a.C; ++c) {
+    const T* Ic = static_cast<const T*>(a.I) + c * a.cs;
+    float* oc = a.coef + c * a.ocs;
+    for (int64_t b = 0; b < g.nbc; b += g.per) {
+      const int64_t n = g.nbc - b < g.per ? g.nbc - b : g.per;
+      const int64_t waves = contig ? n : (n + (1 << ulog) - 1) >> ulog;  // waves with work
+      const int64_t wgs = (waves + pl.W - 1) / pl.W;
+      const unsigned grid = (unsigned)(wgs < cus ? wgs : cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * pl.W), pl.lds, a.stream, a.pinv, a.N, Ic, a.P, oc, 64 * b, n,
+                         pl.ring, ulog);
+      ++launches;
+    }
+  }
+  note_launches(launches);
   return RTI_OK;
 }
 
 template <int K, typename T>
-int launch_vstream_k(const PmArgs& a, const VPlan& pl) {
+int launch_vgen_k(const PmArgs& a, const VPlan& pl, int g_req, bool contig) {
   const bool planar = a.layout == RTI_COEF_PLANAR;
   if (a.N % 4 == 0)
-    return planar ? launch_vstream_t<K, T, RTI_COEF_PLANAR, 4>(a, pl) : launch_vstream_t<K, T, RTI_COEF_PIXEL_MAJOR, 4>(a, pl);
-  return planar ? launch_vstream_t<K, T, RTI_COEF_PLANAR, 1>(a, pl) : launch_vstream_t<K, T, RTI_COEF_PIXEL_MAJOR, 1>(a, pl);
+    return planar ? launch_vgen_t<K, T, RTI_COEF_PLANAR, 4>(a, pl, g_req, contig)
+                  : launch_vgen_t<K, T, RTI_COEF_PIXEL_MAJOR, 4>(a, pl, g_req, contig);
+  return planar ? launch_vgen_t<K, T, RTI_COEF_PLANAR, 1>(a, pl, g_req, contig)
+                : launch_vgen_t<K, T, RTI_COEF_PIXEL_MAJOR, 1>(a, pl, g_req, contig);
 }
 
 template <typename T>
-int launch_vstream(const PmArgs& a, const VPlan& pl) {
-  return a.k == 6 ? launch_vstream_k<6, T>(a, pl) : launch_vstream_k<9, T>(a, pl);
-}
-
-// the whole coefficient array must be addressable by 32-bit buffer offsets
-static bool vstream_coef_ok(const PmArgs& a) {
-  return (uint64_t)a.ocs * (a.C - 1) * 4 + (uint64_t)a.P * a.k * 4 < 0xFFFFFFF0ull;
+int launch_vgen(const PmArgs& a, const VPlan& pl, int g_req, bool contig) {
+  return a.k == 6 ? launch_vgen_k<6, T>(a, pl, g_req, contig) : launch_vgen_k<9, T>(a, pl, g_req, contig);
 }
 
 // DIRECT plan: NS 16-light steps (a bucket >= ceil(N / 16): the extra steps' loads are out of range, no bytes),
@@ -1029,7 +1038,8 @@ template <int K, typename T, int LAYOUT, int NS>
 int launch_direct_t(const PmArgs& a, const DirectOpts& o) {
   constexpr int D = pm_direct_depth(NS), RPX = 16 * pm_direct_run<K, NS>();
   const int64_t ngrp = (a.P + 15) / 16, nrun = (a.P + RPX - 1) / RPX, tr = nrun * a.C;
-  if (ngrp >= ((int64_t)1 << 31) - 4096 || a.P * K * 4 >= ((int64_t)1 << 31))
+  // the kernel's run and group cursors are 32-bit (first = r0 + gw, runs < tr + GW)
+  if (ngrp >= ((int64_t)1 << 31) - 4096 || tr >= ((int64_t)1 << 31) - 65536 || a.P * K * 4 >= ((int64_t)1 << 31))
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: P too large");
   auto kern = fit_pm_direct<K, T, LAYOUT, NS, D>;
   if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR)
@@ -1100,37 +1110,76 @@ void launch_lane(const PmArgs& a) {
 
 using namespace rti;
 
-// the shapes the DMA/MFMA kernels take (both forms)
-static bool pm_dma_shape(int k, int N, int in_dtype, int64_t P, int C, int64_t ps, int64_t cs) {
+// the shapes the DMA / MFMA kernels take: F32 / I32, pixel stride N, 16-byte aligned pixel runs and channels
+// (P·N and the channel stride multiples of 4); `lim32`: the forms whose coefficient offsets are 32-bit
+// (every form but the VALU generations) also need P·k·4 < 2^31
+static bool pm_dma_shape(int k, int N, int in_dtype, int64_t P, int C, int64_t ps, int64_t cs, bool lim32) {
   if (k != 6 && k != 9 && k != 16) return false;
   if (in_dtype != RTI_F32 && in_dtype != RTI_I32) return false;
-  return ps == N && (P * N) % 4 == 0 && (C <= 1 || cs % 4 == 0) && P * (int64_t)k * 4 < ((int64_t)1 << 31);
+  return ps == N && (P * N) % 4 == 0 && (C <= 1 || cs % 4 == 0) && (!lim32 || P * (int64_t)k * 4 < ((int64_t)1 << 31));
+}
+
+// the kernel-selection bits rti_fit_shared_pm accepts: the selector (AUTO / VALU / MFMA / TILE) and the tuning
+// fields of include/rti.h that it documents; anything else is RTI_ERR_BAD_ARG
+static constexpr int PM_FLAGS = RTI_KERNEL_STAGE | RTI_KERNEL_NT_STORE | RTI_KERNEL_ROTATE |
+                                (0xF << RTI_KERNEL_CHUNKS_SHIFT) | (0xF << RTI_KERNEL_TILE_WAVES_SHIFT);
+
+static bool pm_flags_ok(int kernel) {
+  const int sel = kernel & 0xff;
+  return sel <= RTI_KERNEL_TILE && (kernel & ~0xff & ~PM_FLAGS) == 0;
+}
+
+// the form AUTO / the selector picks (0: one lane per pixel); `size` and `w` as rti_fit_shared_pm_plan reports them
+static int pm_choose(int k, int N, int in_dtype, int64_t P, int C, int64_t ps, int64_t cs, int kernel, int* size,
+                     int* w) {
+  const int sel = kernel & 0xff;
+  const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
+  const bool stage = (kernel & RTI_KERNEL_STAGE) != 0;
+  const size_t es = 4;
+  if (sel == RTI_KERNEL_VALU || !pm_dma_shape(k, N, in_dtype, P, C, ps, cs, false)) return 0;
+  if (sel == RTI_KERNEL_AUTO && !stage) {
+    const VPlan vp = vgen_plan(k, N, es, w_req);
+    if (vp.W) {
+      *size = vp.ring >> 10;
+      *w = vp.W;
+      return RTI_PM_VALU_STREAM;
+    }
+  }
+  if (!pm_dma_shape(k, N, in_dtype, P, C, ps, cs, true)) return 0;
+  if (sel == RTI_KERNEL_AUTO && N % 4 == 0 && pm_direct_ns(N)) {
+    *size = pm_direct_ns(N);
+    *w = w_req ? w_req : PM_DIRECT_WPC;
+    return RTI_PM_DIRECT;
+  }
+  if (sel != RTI_KERNEL_TILE) {
+    const StreamPlan sp = stream_plan(N, es, w_req, c_req);
+    if (sp.W) {
+      *size = sp.ring >> 10;
+      *w = sp.W;
+      return RTI_PM_MFMA_STREAM;
+    }
+  }
+  const PmPlan pl = pm_plan(N, es, sel == RTI_KERNEL_TILE ? c_req : 0, w_req);
+  if (!pl.G) return 0;
+  *size = 16 * pl.G;
+  *w = pl.W;
+  return RTI_PM_BLOCK;
 }
 
 extern "C" int rti_fit_shared_pm_plan(int k, int N, int in_dtype, int64_t P, int C, int64_t pixel_stride,
                                       int64_t channel_stride, int kernel) {
+  if (!pm_flags_ok(kernel) || N <= 0 || P <= 0 || C <= 0) return 0;
   const int64_t ps = pixel_stride ? pixel_stride : N;
   const int64_t cs = channel_stride ? channel_stride : P * ps;
-  if (!pm_dma_shape(k, N, in_dtype, P, C, ps, cs) || (kernel & 0xff) == RTI_KERNEL_VALU) return 0;
-  const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
-  const bool stage = (kernel & RTI_KERNEL_STAGE) != 0;
-  if ((kernel & 0xff) == RTI_KERNEL_AUTO && !stage) {
-    const VPlan vp = vstream_plan(k, N, 4, w_req);
-    if (vp.W && (int64_t)C * P * k * 4 < 0xFFFFFFF0ll) return RTI_PM_VALU_STREAM * 100000000 + (vp.ring >> 10) * 1000 + vp.W;
-  }
-  if ((kernel & 0xff) == RTI_KERNEL_AUTO && N % 4 == 0 && pm_direct_ns(N))
-    return RTI_PM_DIRECT * 100000000 + pm_direct_ns(N) * 1000 + (w_req ? w_req : PM_DIRECT_WPC);
-  if ((kernel & 0xff) != RTI_KERNEL_TILE) {
-    const StreamPlan sp = stream_plan(N, 4, w_req, c_req);
-    if (sp.W) return RTI_PM_MFMA_STREAM * 100000000 + (sp.ring >> 10) * 1000 + sp.W;
-  }
-  const PmPlan pl = pm_plan(N, 4, (kernel & 0xff) == RTI_KERNEL_TILE ? c_req : 0, w_req);
-  return pl.G ? RTI_PM_BLOCK * 100000000 + 16 * pl.G * 1000 + pl.W : 0;
+  int size = 0, w = 0;
+  const int form = pm_choose(k, N, in_dtype, P, C, ps, cs, kernel, &size, &w);
+  return form ? form * 100000000 + size * 1000 + w : 0;
 }
 
 extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
                                  int64_t pixel_stride, int64_t channel_stride, float* coef, int coef_layout,
                                  int64_t coef_channel_stride, int kernel, rti_stream_t stream) {
+  if (!pm_flags_ok(kernel)) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: unknown kernel bits 0x%x", kernel);
   if (!pinv || !I || !coef) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: null pointer");
   if (N <= 0 || P <= 0 || C <= 0 || C > 65535) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: bad N/P/C");
   if (k < 1 || k > 16) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: k=%d outside 1..16", k);
@@ -1152,54 +1201,55 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
   a.layout = coef_layout;
   a.ocs = coef_channel_stride ? coef_channel_stride : P * k;
   a.stream = (hipStream_t)stream;
-  a.mode = (kernel & RTI_KERNEL_ONE_LAUNCH) ? 1 : (kernel & RTI_KERNEL_ROUNDS) ? 2 : (kernel & RTI_KERNEL_PINV_LDS) ? 3 : 0;
   if (a.ps < N) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: pixel_stride < N");
   if (C > 1 && a.cs < P * a.ps) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: channel_stride");
   if (C > 1 && a.ocs < P * k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_pm: coef_channel_stride");
   note_launches(1);
   const int sel = kernel & 0xff;
-  const size_t es = in_dtype == RTI_U8 ? 1 : 4;
-  const bool dma_ok = sel != RTI_KERNEL_VALU &&
-                      rti_fit_shared_pm_plan(k, N, in_dtype, P, C, a.ps, a.cs, kernel) != 0 &&
-                      aligned_to(I, 16) && aligned_to(coef, 16) && a.ocs % 4 == 0;
   const int w_req = (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF, c_req = (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF;
-  // AUTO: k <= 9 the VALU stream (one pixel per lane, packed FMAs: c3 0.645 ms against 0.682 direct), k = 16
-  // the direct form (c4 3.754 against 3.858 ms for the MFMA stream; profiles/r04r_pm_sweep_c*.log);
-  // RTI_KERNEL_STAGE with AUTO forces the direct form (its coefficients are staged through LDS)
-  if (dma_ok && sel == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE)) {
-    const VPlan vp = vstream_plan(k, N, es, w_req);
-    if (vp.W && vstream_coef_ok(a)) {
-      const int st = in_dtype == RTI_F32 ? launch_vstream<float>(a, vp) : launch_vstream<int32_t>(a, vp);
-      return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
+  int size = 0, w = 0;
+  int form = pm_choose(k, N, in_dtype, P, C, a.ps, a.cs, kernel, &size, &w);
+  // the VALU generations store per lane (float2 pairs for even k, pixel-major): 8-byte aligned channels; the
+  // other forms' buffer stores and LDS bursts want 16-byte aligned coefficient rows
+  const bool coef_ok = form == RTI_PM_VALU_STREAM ? aligned_to(coef, 8) && a.ocs % 2 == 0
+                                                  : aligned_to(coef, 16) && a.ocs % 4 == 0;
+  if (!(aligned_to(I, 16) && coef_ok)) form = 0;
+  const bool i32 = in_dtype == RTI_I32;
+  int st = RTI_OK;
+  switch (form) {
+    case RTI_PM_VALU_STREAM: {  // AUTO, k <= 9 (c3: 0.55 ms, §4.1f)
+      const VPlan vp = vgen_plan(k, N, 4, w_req);
+      const bool contig = (kernel & RTI_KERNEL_ROTATE) != 0;  // each wave one contiguous run (A/B)
+      st = i32 ? launch_vgen<int32_t>(a, vp, c_req, contig) : launch_vgen<float>(a, vp, c_req, contig);
+      break;
     }
-  }
-  if (dma_ok && sel == RTI_KERNEL_AUTO && N % 4 == 0 && pm_direct_ns(N)) {
-    DirectOpts o;  // straight to registers.  Measurement flags: TILE_WAVES(w) waves per CU, CHUNKS(n) launch
-    if (w_req) o.wpc = w_req;  // generations, NT_STORE non-temporal bursts
-    if (c_req) o.gens = c_req;
-    o.nts = (kernel & RTI_KERNEL_NT_STORE) != 0;
-    const int st = in_dtype == RTI_F32 ? launch_direct<float>(a, o) : launch_direct<int32_t>(a, o);
-    return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
-  }
-  if (dma_ok) {
-    StreamPlan sp;
-    if (sel != RTI_KERNEL_TILE) sp = stream_plan(N, es, w_req, c_req);
-    int st;
-    if (sp.W) {  // AUTO / MFMA: the streaming ring
-      sp.contig = (kernel & RTI_KERNEL_ROTATE) != 0;  // measurement: each wave one contiguous run of units
-      st = in_dtype == RTI_F32 ? launch_stream<float>(a, sp) : launch_stream<int32_t>(a, sp);
-    } else {  // the double-buffered block form (kernel TILE, or N < 16)
-      const PmPlan pl = pm_plan(N, es, sel == RTI_KERNEL_TILE ? c_req : 0, w_req);
-      st = in_dtype == RTI_F32 ? launch_dma<float>(a, pl) : launch_dma<int32_t>(a, pl);
+    case RTI_PM_DIRECT: {  // AUTO k = 16, AUTO | STAGE: straight to registers.  Measurement flags:
+      DirectOpts o;        // TILE_WAVES(w) waves per CU, CHUNKS(n) launch generations, NT_STORE non-temporal bursts
+      if (w_req) o.wpc = w_req;
+      if (c_req) o.gens = c_req;
+      o.nts = (kernel & RTI_KERNEL_NT_STORE) != 0;
+      st = i32 ? launch_direct<int32_t>(a, o) : launch_direct<float>(a, o);
+      break;
     }
-    return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
+    case RTI_PM_MFMA_STREAM: {  // RTI_KERNEL_MFMA: the MFMA stream through the LDS ring
+      StreamPlan sp = stream_plan(N, 4, w_req, c_req);
+      sp.contig = (kernel & RTI_KERNEL_ROTATE) != 0;  // each wave one contiguous run of units
+      st = i32 ? launch_stream<int32_t>(a, sp) : launch_stream<float>(a, sp);
+      break;
+    }
+    case RTI_PM_BLOCK: {  // RTI_KERNEL_TILE (or N too small for a ring): the double-buffered block form
+      const PmPlan pl = pm_plan(N, 4, sel == RTI_KERNEL_TILE ? c_req : 0, w_req);
+      st = i32 ? launch_dma<int32_t>(a, pl) : launch_dma<float>(a, pl);
+      break;
+    }
+    default:
+      if (sel == RTI_KERNEL_MFMA || sel == RTI_KERNEL_TILE)
+        return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: the DMA/MFMA kernels do not take this shape");
+      switch (in_dtype) {
+        case RTI_F32: launch_lane<float>(a); break;
+        case RTI_I32: launch_lane<int32_t>(a); break;
+        default: launch_lane<uint8_t>(a); break;
+      }
   }
-  if (sel == RTI_KERNEL_MFMA || sel == RTI_KERNEL_TILE)
-    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_pm: the DMA/MFMA kernels do not take this shape");
-  switch (in_dtype) {
-    case RTI_F32: launch_lane<float>(a); break;
-    case RTI_I32: launch_lane<int32_t>(a); break;
-    default: launch_lane<uint8_t>(a); break;
-  }
-  return check_launch("rti_fit_shared_pm");
+  return st != RTI_OK ? st : check_launch("rti_fit_shared_pm");
 }

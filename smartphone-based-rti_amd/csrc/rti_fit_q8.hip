@@ -289,6 +289,8 @@ extern "C" int rti_fit_shared_q8_max_lights(void) {
 extern "C" int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I, int64_t P, int C,
                                  int64_t light_stride, int64_t channel_stride, float* coef, int coef_layout,
                                  int64_t coef_channel_stride, int kernel, rti_stream_t stream) {
+  if (!kernel_bits_ok(kernel, RTI_KERNEL_AUTO, RTI_KERNEL_STAGE | RTI_FIELD_CHUNKS | RTI_FIELD_TILE_DEPTH))
+    return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_q8: unknown kernel bits 0x%x", kernel);
   if (!op || !I || !coef) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_q8: null pointer");
   if (N <= 0 || P <= 0 || C <= 0 || C > 65535) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_q8: bad N/P/C");
   if (N < k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_q8: N=%d < k=%d", N, k);

@@ -319,6 +319,8 @@ int fit_shared_residual_impl(bool orth, const double* A, const double* ginv, int
                              int64_t P, int C, int64_t light_stride, int64_t channel_stride, float* coef,
                              int coef_layout, int64_t coef_channel_stride, float* res, double* partial, int kernel,
                              rti_stream_t stream) {
+  if (!kernel_bits_ok(kernel, RTI_KERNEL_AUTO, RTI_KERNEL_ONE_LAUNCH | RTI_FIELD_CHUNKS))
+    return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: unknown kernel bits 0x%x", kernel);
   if (!A || !ginv || !I || !coef) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: null pointer");
   if (N <= 0 || P <= 0 || C <= 0 || C > 65535) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: bad N/P/C");
   if (N < k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_residual: N=%d < k=%d", N, k);

@@ -19,6 +19,17 @@ int device_cus();
 // records the kernel launches of the current C-ABI call (rti_last_launch_count)
 void note_launches(int n);
 
+// A kernel-selection word: selector (low byte) <= max_sel and no bit outside `flags`.  Every entry point that
+// takes one refuses anything else with RTI_ERR_BAD_ARG, so no bit a caller passes can select a behaviour the
+// entry does not document (tests/test_abi.py::test_entry_points_refuse_unknown_kernel_bits).
+inline bool kernel_bits_ok(int kernel, int max_sel, int flags) {
+  return (kernel & 0xff) <= max_sel && (kernel & ~0xff & ~flags) == 0;
+}
+constexpr int RTI_FIELD_CHUNKS = 0xF << RTI_KERNEL_CHUNKS_SHIFT;
+constexpr int RTI_FIELD_TILE_PLANES = 0xF << RTI_KERNEL_TILE_PLANES_SHIFT;
+constexpr int RTI_FIELD_TILE_DEPTH = 0xF << RTI_KERNEL_TILE_DEPTH_SHIFT;
+constexpr int RTI_FIELD_TILE_WAVES = 0xF << RTI_KERNEL_TILE_WAVES_SHIFT;
+
 __host__ __device__ inline bool aligned_to(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
 inline unsigned grid_1d(int64_t items, int per_block) { return (unsigned)((items + per_block - 1) / per_block); }

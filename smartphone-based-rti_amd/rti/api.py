@@ -188,8 +188,14 @@ def fit_q8_into(op_dev, I, coef, *, k, layout="pixel", flags=0):
     return coef
 
 
+_PM_KERNELS = ("auto", "valu", "mfma", "tile")  # the selectors rti_fit_shared_pm honours
+
+
 def _fit_shared_pixel_major(I, lu, lv, b, k, rcond, cl, kernel, given_pixel_major):
     """rti.fit(mode="shared") on a pixel-major stack: ``rti_fit_shared_pm`` on the tensor's own memory."""
+    if kernel not in _PM_KERNELS:
+        raise NotImplementedError(f"kernel={kernel!r} does not take pixel-major stacks (rti_fit_shared_pm: "
+                                  f"{', '.join(_PM_KERNELS)}); pass stack='light' with a light-major stack")
     if given_pixel_major:
         if I.dim() == 2:
             spatial, C = (I.shape[0],), 1
@@ -220,9 +226,8 @@ def _fit_shared_pixel_major(I, lu, lv, b, k, rcond, cl, kernel, given_pixel_majo
         raise ValueError(f"I dtype {I.dtype} unsupported (float32, uint8 or int32)")
     coef = torch.empty((C, P, k) if cl == L.RTI_COEF_PIXEL_MAJOR else (C, k, P), dtype=torch.float32,
                        device=I.device)
-    kern = kernel if kernel in ("auto", "mfma", "valu") else "auto"
     fit_shared_pm_into(torch.as_tensor(pv.astype(np.float32), device=I.device), v, coef, k=k, layout=cl,
-                       kernel=kern)
+                       kernel=kernel)
     out = coef.reshape((C,) + spatial + (k,)) if cl == L.RTI_COEF_PIXEL_MAJOR else coef.reshape((C, k) + spatial)
     return out if lead4 else out[0]
 
@@ -281,11 +286,14 @@ def fit_shared_pm_into(pinv_dev, I, coef, *, k, layout="pixel", kernel="auto", f
     """Launch ``rti_fit_shared_pm`` (pixel-major stacks, the reference's (R, R, N) layout,
     analysis.py:217-219) on preallocated tensors: pinv_dev CUDA fp32 [k, N]; I CUDA [P, N] or [C, P, N]
     with unit light stride (any pixel / channel stride, e.g. a view of [H, W, N]); coef as
-    fit_shared_into."""
+    fit_shared_into.  A broadcast (stride-0) pixel or channel dimension is materialised first: the C ABI
+    reads a zero stride as "dense"."""
     I3 = I if I.dim() == 3 else I.unsqueeze(0)
     C, P, N = I3.shape
     if I3.stride(2) != 1 and N > 1:
         raise ValueError("pixel-major stack needs unit light stride (I[..., p, n] with n contiguous)")
+    if (P > 1 and I3.stride(1) == 0) or (C > 1 and I3.stride(0) == 0):
+        I3 = I3.contiguous()
     ps = I3.stride(1) if P > 1 else N
     cs = I3.stride(0) if C > 1 else P * ps
     kern = _KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
@@ -301,6 +309,8 @@ def _pixel_major_of(I):
     (I.permute of the reference's [H, W, N]) -> the same data as [C, P, N] with unit light stride, else None."""
     if I.dim() < 2 or I.dim() > 4 or I.stride(1 if I.dim() == 4 else 0) != 1:
         return None  # the light dimension must be the unit-stride one
+    if any(st == 0 and n > 1 for st, n in zip(I.stride(), I.shape)):
+        return None  # a broadcast (expanded) dimension: not a pixel-major stack in memory
     if I.dim() == 2:
         v = I.t().unsqueeze(0)
     elif I.dim() == 3:
@@ -326,8 +336,9 @@ def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=Non
         I: CUDA tensor [N, H, W], [N, P] or [C, N, H, W] (light-major), fp32/u8/int32;
         with stack="pixel" the reference's own pixel-major layout instead, [H, W, N], [P, N] or
         [C, H, W, N] (analysis.py:217-219), fitted in place by ``rti_fit_shared_pm`` (no transpose).
-        stack="auto" also routes a light-major-shaped VIEW of a pixel-major stack (``Ipm.permute(2, 0, 1)``)
-        to that kernel instead of copying it.
+        stack="auto" also routes a light-major-shaped VIEW of an fp32 / int32 pixel-major stack
+        (``Ipm.permute(2, 0, 1)``) to that kernel instead of copying it, when kernel is one it takes
+        ("auto", "valu", "mfma", "tile") and nontemporal is off; 8-bit views keep the copy + h16 path.
         lu, lv: N light directions (host or device).  Returns fp32 coefficients
         [.., H, W, k] (layout="pixel") or [.., k, H, W] (layout="planar").
         uint8 light-major stacks run the split-fp16 MFMA kernel under kernel="auto" (``rti_fit_shared_h16``:
@@ -348,8 +359,16 @@ def fit(I, lu=None, lv=None, basis="ptm", mode="shared", rcond=None, *, cams=Non
         k = basis_terms(b)
         if stack not in ("auto", "light", "pixel"):
             raise ValueError(f"unknown stack layout {stack!r} (expected 'auto', 'light' or 'pixel')")
-        if stack == "pixel" or (stack == "auto" and not I.is_contiguous() and _pixel_major_of(I) is not None):
-            return _fit_shared_pixel_major(I, lu, lv, b, k, rcond, cl, kernel, stack == "pixel")
+        if stack == "pixel":
+            if nontemporal:
+                raise NotImplementedError("nontemporal loads apply to light-major stacks (rti_fit_shared)")
+            return _fit_shared_pixel_major(I, lu, lv, b, k, rcond, cl, kernel, True)
+        # AUTO routes a pixel-major VIEW to rti_fit_shared_pm only where that kernel honours the request: fp32 /
+        # int32 stacks (8-bit stacks keep the transposing copy and the h16 matrix-core fit) and the selectors and
+        # options rti_fit_shared_pm takes; everything else keeps the light-major path below
+        if (stack == "auto" and not I.is_contiguous() and I.dtype in (torch.float32, torch.int32)
+                and kernel in _PM_KERNELS and not nontemporal and _pixel_major_of(I) is not None):
+            return _fit_shared_pixel_major(I, lu, lv, b, k, rcond, cl, kernel, False)
         lead = I.shape[:-2] if I.dim() >= 3 else I.shape[:-1]
         if I.dim() == 2:
             N, P = I.shape

@@ -92,7 +92,7 @@ def fit_rowtiled(I_rows, lu, lv, H, basis="ptm", rcond=None, gather=True, group=
 
 
 def gather_rows_pipelined(produce, h_local, H, trail, dtype, device, chunks=4, group=None, partition="block",
-                          out=None):
+                          out=None, channels=None):
     """All-gather a row-tiled map while it is being produced (overlap the coefficient
     all-gather with fitting).
 
@@ -102,29 +102,41 @@ def gather_rows_pipelined(produce, h_local, H, trail, dtype, device, chunks=4, g
     runs on the communicator's stream — ordered after the kernel that produced it — while the current
     stream produces chunk c + 1.
 
+    channels=C: ``produce`` returns [C, c1 - c0, *trail] (every channel's rows of the chunk, one fit
+    launch) and the map is [C, H, *trail]; each channel's rows are gathered by their own collective.
+
     partition="cyclic": this rank's local rows are its cyclic_rows(H, G, r, chunks) blocks in order;
     every chunk is gathered straight into its place in the [H, *trail] map.
     partition="block": local rows = row_range(H, G, r); with G | H and chunks | H/G each chunk is
     gathered into a staging buffer and moved into place by one strided copy; other shapes pad.
-    Returns the full [H, *trail] map."""
+    Returns the full [H, *trail] (or [C, H, *trail]) map."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     nccl = _nccl(group)
-    full = out if out is not None else torch.empty((H,) + tuple(trail), dtype=dtype, device=device)
+    trail = tuple(trail)
+    C = 1 if channels is None else int(channels)
+    lead = () if channels is None else (C,)
+    full = out if out is not None else torch.empty(lead + (H,) + trail, dtype=dtype, device=device)
+    fullc = full.unsqueeze(0) if channels is None else full  # [C, H, *trail]
+
+    def parts_of(part):  # the chunk's rows per channel
+        return [part] if channels is None else [part[c] for c in range(C)]
+
     if partition == "cyclic":
         blocks = cyclic_rows(H, world, rank, chunks)
         hc = blocks[0][1] - blocks[0][0]
         if h_local != hc * chunks:
             raise ValueError(f"rank {rank} holds {h_local} rows, the cyclic partition gives {hc * chunks}")
         pending = []
-        for c in range(chunks):
-            part = produce(c * hc, (c + 1) * hc)
-            dst = full[c * world * hc:(c + 1) * world * hc]
-            if nccl:
-                pending.append(dist.all_gather_into_tensor(dst, part, group=group, async_op=True))
-            else:
-                host = [torch.empty((hc,) + tuple(trail), dtype=dtype) for _ in range(world)]
-                pending.append((dist.all_gather(host, part.cpu(), group=group, async_op=True), host, dst))
+        for j in range(chunks):
+            part = produce(j * hc, (j + 1) * hc)
+            for c, pc in enumerate(parts_of(part)):
+                dst = fullc[c][j * world * hc:(j + 1) * world * hc]
+                if nccl:
+                    pending.append(dist.all_gather_into_tensor(dst, pc.contiguous(), group=group, async_op=True))
+                else:
+                    host = [torch.empty((hc,) + trail, dtype=dtype) for _ in range(world)]
+                    pending.append((dist.all_gather(host, pc.cpu(), group=group, async_op=True), host, dst))
         for p in pending:
             if nccl:
                 p.wait()
@@ -143,78 +155,184 @@ def gather_rows_pipelined(produce, h_local, H, trail, dtype, device, chunks=4, g
     even = H % world == 0 and (H // world) % chunks == 0
     cmax = -(-hmax // chunks)
     pending = []
-    for c in range(chunks):
-        c0, c1 = row_range(h_local, chunks, c)
+    for j in range(chunks):
+        c0, c1 = row_range(h_local, chunks, j)
         if even:
-            part = produce(c0, c1)
+            pcs = parts_of(produce(c0, c1))
         else:
-            part = torch.zeros((cmax,) + tuple(trail), dtype=dtype, device=device)
+            pad = torch.zeros(lead + (cmax,) + trail, dtype=dtype, device=device)
             if c1 > c0:
-                part[: c1 - c0] = produce(c0, c1)
-        if nccl:
-            buf = torch.empty((world,) + tuple(part.shape), dtype=dtype, device=device)
-            pending.append((dist.all_gather_into_tensor(buf.view((-1,) + tuple(trail)), part, group=group,
-                                                        async_op=True), buf))
-        else:
-            host = part.cpu()
-            bufs = [torch.empty_like(host) for _ in range(world)]
-            pending.append((dist.all_gather(bufs, host, group=group, async_op=True), bufs))
+                pad.narrow(len(lead), 0, c1 - c0).copy_(produce(c0, c1))
+            pcs = parts_of(pad)
+        for c, part in enumerate(pcs):
+            part = part.contiguous()
+            if nccl:
+                buf = torch.empty((world,) + tuple(part.shape), dtype=dtype, device=device)
+                pending.append((c, j, dist.all_gather_into_tensor(buf.view((-1,) + trail), part, group=group,
+                                                                  async_op=True), buf))
+            else:
+                host = part.cpu()
+                bufs = [torch.empty_like(host) for _ in range(world)]
+                pending.append((c, j, dist.all_gather(bufs, host, group=group, async_op=True), bufs))
     hb = H // world if even else None
-    for c, (work, parts) in enumerate(pending):
+    for c, j, work, parts in pending:
         work.wait()
         if not nccl:
             parts = torch.stack(parts).to(device)
-        if even:  # one strided copy: rank r's chunk c -> rows r·hb + [c0, c1)
-            c0, c1 = row_range(hb, chunks, c)
-            full.view((world, hb) + tuple(trail))[:, c0:c1] = parts
+        if even:  # one strided copy: rank r's chunk j -> rows r·hb + [c0, c1)
+            c0, c1 = row_range(hb, chunks, j)
+            fullc[c].view((world, hb) + trail)[:, c0:c1] = parts
             continue
         for r in range(world):
             h_r = rows[r][1] - rows[r][0]
-            c0, c1 = row_range(h_r, chunks, c)
-            full[rows[r][0] + c0:rows[r][0] + c1] = parts[r][: c1 - c0].to(device)
+            c0, c1 = row_range(h_r, chunks, j)
+            fullc[c][rows[r][0] + c0:rows[r][0] + c1] = parts[r][: c1 - c0].to(device)
     return full
 
 
+def local_to_global_row(H, world, rank, chunks, partition, c0):
+    """Global image row of local row c0 at the start of a produced chunk (the row origin a per-pixel
+    fit needs: analysis.py:228 takes p = (x, y, 0) in whole-image indices)."""
+    if partition == "cyclic":
+        blocks = cyclic_rows(H, world, rank, chunks)
+        hc = blocks[0][1] - blocks[0][0]
+        j, off = divmod(c0, hc)
+        return blocks[j][0] + off
+    return row_range(H, world, rank)[0] + c0
+
+
 class RowTiledFitter:
-    """Row-tiled shared fit of this rank's rows with the all-gather of each row chunk overlapped with
-    the fit of the next (one rti_fit_shared launch per chunk on the current stream).  The pseudo-
-    inverse, the local coefficient rows and the full map are allocated once; ``__call__`` returns the
-    full [H, W, k] map (the same tensor every call).
+    """Row-tiled fit of this rank's rows with the all-gather of each row chunk overlapped with the fit of
+    the next (one fit launch per chunk, all channels, on the current stream).  The operator, the local
+    coefficient rows and the full map are allocated once; ``__call__`` returns the full map (the same
+    tensor every call): [H, W, k] for one channel, [C, H, W, k] for C (every pixel is
+    independent, the only exchange is the coefficient all-gather).
 
-    I_rows: this rank's CUDA light-major rows [N, h, W] (block partition: rows row_range(H, G, r);
-    cyclic: its cyclic_rows(H, G, r, chunks) blocks in order)."""
+    I_rows: this rank's CUDA rows (block partition: rows row_range(H, G, r); cyclic: its
+    cyclic_rows(H, G, r, chunks) blocks in order), in any form rti.fit takes:
+      * mode="shared", stack="light": light-major [N, h, W] or [C, N, h, W], fp32 / int32 / uint8; 8-bit
+        stacks run the split-fp16 matrix-core fit (rti_fit_shared_h16, rti.fit's AUTO) when W is a
+        multiple of 16, else rti_fit_shared;
+      * mode="shared", stack="pixel": the reference's pixel-major [h, W, N] or [C, h, W, N]
+        (analysis.py:217-219), fitted in place by rti_fit_shared_pm;
+      * mode="perpixel" (PTM-6): cams [N, 3] and light-major [N, h, W]; each chunk's light vectors use its
+        rows' GLOBAL image indices (rti_fit_perpixel_cam with the chunk's row origin, analysis.py:228), so
+        the gathered map equals the whole-image fit; coef_dtype fp32 or fp64."""
 
-    def __init__(self, I_rows, lu, lv, H, basis="ptm", rcond=None, chunks=4, group=None, kernel="auto",
-                 partition="block"):
+    def __init__(self, I_rows, lu=None, lv=None, H=None, basis="ptm", rcond=None, chunks=4, group=None,
+                 kernel="auto", partition="block", stack="light", mode="shared", cams=None, origin=(0.0, 0.0),
+                 coef_dtype=torch.float32):
         api._require_cuda(I_rows, "I_rows")
-        self.N, self.h, self.W = I_rows.shape
+        if H is None:
+            raise ValueError("H (the whole image's rows) is required")
+        if mode not in ("shared", "perpixel"):
+            raise ValueError(f"unknown mode {mode!r}")
+        if stack not in ("light", "pixel"):
+            raise ValueError(f"unknown stack layout {stack!r}")
         self.H, self.chunks, self.group, self.partition = H, chunks, group, partition
-        b = api.basis_id(basis)
-        self.k = api.basis_terms(b)
+        self.mode, self.stack, self.origin = mode, stack, (float(origin[0]), float(origin[1]))
         dev = I_rows.device
-        self.pinv = torch.as_tensor(api.pinv(lu, lv, basis, rcond=rcond).astype(np.float32), device=dev)
         self.I = I_rows.contiguous()
-        self.coef = torch.empty((self.h, self.W, self.k), dtype=torch.float32, device=dev)
-        self.full = torch.empty((H, self.W, self.k), dtype=torch.float32, device=dev)
-        self.kern = api._KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+        if mode == "perpixel":
+            if api.basis_id(basis) != L.RTI_BASIS_PTM6 or stack != "light" or self.I.dim() != 3:
+                raise ValueError("per-pixel row tiling: PTM-6, light-major [N, h, W] rows and cams")
+            self.C, (self.N, self.h, self.W) = 1, self.I.shape
+            self.k = 6
+            self.cdt = api._COEF_DTYPES.get(coef_dtype)
+            if self.cdt is None:
+                raise ValueError("coef_dtype must be torch.float32 or torch.float64")
+            cams_np = np.asarray(cams.detach().cpu() if torch.is_tensor(cams) else cams, np.float64)
+            self.cams = torch.as_tensor(cams_np, device=dev).contiguous()
+            if self.cams.shape != (self.N, 3):
+                raise ValueError(f"cams must be [{self.N}, 3]")
+            self.rc = -1.0 if rcond is None else float(rcond)
+            self.dtype = coef_dtype
+        else:
+            if lu is None or lv is None:
+                raise ValueError("shared mode needs lu and lv")
+            if stack == "light":
+                x = self.I if self.I.dim() == 4 else self.I.unsqueeze(0)
+                self.C, self.N, self.h, self.W = x.shape
+            else:
+                x = self.I if self.I.dim() == 4 else self.I.unsqueeze(0)
+                self.C, self.h, self.W, self.N = x.shape
+            b = api.basis_id(basis)
+            self.k = api.basis_terms(b)
+            pv = api.pinv(lu, lv, basis, rcond=rcond)
+            if pv.shape[1] != self.N:
+                raise ValueError(f"{pv.shape[1]} light directions for {self.N} intensity planes")
+            self.pinv = torch.as_tensor(pv.astype(np.float32), device=dev)
+            self.kern = api._KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+            self.dtype = torch.float32
+            self.h16 = None
+            if (stack == "light" and self.I.dtype == torch.uint8 and kernel == "auto" and self.W % 16 == 0
+                    and self.k in (6, 9, 16) and self.N <= int(L.lib().rti_fit_shared_h16_max_lights())
+                    and np.isfinite(pv).all() and self.I.data_ptr() % 16 == 0):
+                self.h16 = torch.as_tensor(api.h16_operator(pv), device=dev)
         self.dt = api._IN_DTYPES[self.I.dtype]
+        self.coef = torch.empty((self.C, self.h, self.W, self.k), dtype=self.dtype, device=dev)
+        lead = (self.C,) if self.C > 1 or self.I.dim() == 4 else ()
+        self.full = torch.empty(lead + (H, self.W, self.k), dtype=self.dtype, device=dev)
+        self.channels = self.C if lead else None
 
     def _produce(self, c0, c1):
-        W, k, N, es = self.W, self.k, self.N, self.I.element_size()
-        st = L.lib().rti_fit_shared(api._vp(self.pinv), k, N, self.I.data_ptr() + c0 * W * es, self.dt,
-                                    (c1 - c0) * W, 1, self.h * W, 0, self.coef.data_ptr() + c0 * W * k * 4,
-                                    L.RTI_COEF_PIXEL_MAJOR, 0, self.kern, api._stream_of(self.I))
-        L.check(st, "rti_fit_shared")
-        return self.coef[c0:c1]
+        W, k, N, C, h = self.W, self.k, self.N, self.C, self.h
+        es, ces = self.I.element_size(), self.coef.element_size()
+        P = (c1 - c0) * W
+        s = api._stream_of(self.I)
+        ocs = h * W * k
+        dst = self.coef.data_ptr() + c0 * W * k * ces
+        lib = L.lib()
+        if self.mode == "perpixel":
+            world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
+            y0 = local_to_global_row(self.H, world, rank, self.chunks, self.partition, c0)
+            st = lib.rti_fit_perpixel_cam(api._vp(self.cams), N, self.I.data_ptr() + c0 * W * es, self.dt, c1 - c0,
+                                          W, h * W, self.origin[0], self.origin[1] + y0, self.rc, dst, self.cdt,
+                                          L.RTI_COEF_PIXEL_MAJOR, s)
+            L.check(st, "rti_fit_perpixel_cam")
+        elif self.stack == "pixel":
+            st = lib.rti_fit_shared_pm(api._vp(self.pinv), k, N, self.I.data_ptr() + c0 * W * N * es, self.dt, P, C,
+                                       N, h * W * N, dst, L.RTI_COEF_PIXEL_MAJOR, ocs, self.kern & 0xff, s)
+            L.check(st, "rti_fit_shared_pm")
+        elif self.h16 is not None:
+            st = lib.rti_fit_shared_h16(api._vp(self.h16), k, N, self.I.data_ptr() + c0 * W, P, C, h * W, N * h * W,
+                                        dst, L.RTI_COEF_PIXEL_MAJOR, ocs, 0, s)
+            L.check(st, "rti_fit_shared_h16")
+        else:
+            st = lib.rti_fit_shared(api._vp(self.pinv), k, N, self.I.data_ptr() + c0 * W * es, self.dt, P, C, h * W,
+                                    N * h * W, dst, L.RTI_COEF_PIXEL_MAJOR, ocs, self.kern, s)
+            L.check(st, "rti_fit_shared")
+        return self.coef[:, c0:c1] if self.channels else self.coef[0, c0:c1]
 
     def __call__(self):
-        return gather_rows_pipelined(self._produce, self.h, self.H, (self.W, self.k), torch.float32,
+        return gather_rows_pipelined(self._produce, self.h, self.H, (self.W, self.k), self.dtype,
                                      self.I.device, chunks=self.chunks, group=self.group,
-                                     partition=self.partition, out=self.full)
+                                     partition=self.partition, out=self.full, channels=self.channels)
 
 
-def fit_rowtiled_overlapped(I_rows, lu, lv, H, basis="ptm", rcond=None, chunks=4, group=None, kernel="auto",
-                            partition="block"):
-    """One-shot form of RowTiledFitter: returns the full [H, W, k] map on every rank."""
+def fit_rowtiled_overlapped(I_rows, lu=None, lv=None, H=None, basis="ptm", rcond=None, chunks=4, group=None,
+                            kernel="auto", partition="block", **kw):
+    """One-shot form of RowTiledFitter: returns the full map on every rank."""
     return RowTiledFitter(I_rows, lu, lv, H, basis=basis, rcond=rcond, chunks=chunks, group=group, kernel=kernel,
-                          partition=partition)()
+                          partition=partition, **kw)()
+
+
+def gather_evals(local, H, group=None):
+    """[E, h_r, W] relit rows of every rank (block partition) -> the whole [E, H, W] images: the rows are
+    gathered as [h_r, E, W] (rows outermost, so row blocks land in order) and viewed back."""
+    full = gather_rows(local.permute(1, 0, 2).contiguous(), H, group=group)  # [H, E, W]
+    return full.permute(1, 0, 2)
+
+
+def relight_rowtiled(coef_rows, lu, lv, H, basis="ptm", *, gather=False, group=None, out_dtype=torch.float32):
+    """relight is row-shardable.  Every rank evaluates its own coefficient rows
+    [h_r, W, k] (block partition) at the E directions (rti.relight, interactive_relighting.py:11-39 /
+    analysis.py:300-315): no exchange.  gather=True assembles whole [E, H, W] images on every rank (a
+    display), one all-gather."""
+    img = api.relight(coef_rows, lu, lv, basis=basis, out_dtype=out_dtype)
+    scalar = img.dim() == 2
+    loc = img.unsqueeze(0) if scalar else img  # [E, h, W]
+    if not gather:
+        return img
+    full = gather_evals(loc, H, group=group)
+    return full[0] if scalar else full

@@ -230,3 +230,51 @@ def test_h16_operator_rejects_non_finite():
     e = golden("ptm_edge.npz")
     with pytest.raises(ValueError, match="non-finite"):
         rti.h16_operator(rti.pinv(e["singular_lu"], e["singular_lv"]))
+
+
+def test_entry_points_refuse_unknown_kernel_bits():
+    """Every entry point that takes a kernel-selection word refuses bits it does not document with
+    RTI_ERR_BAD_ARG before it touches a pointer (no flag may return RTI_OK with the
+    coefficients unwritten).  The pointers here are never dereferenced: the check comes first."""
+    import ctypes
+
+    lib = rti.load()
+    p = ctypes.c_void_p(4096)
+    calls = {
+        "rti_fit_shared": lambda kern: lib.rti_fit_shared(p, 6, 20, p, L.RTI_F32, 64, 1, 0, 0, p, 0, 0, kern, None),
+        "rti_fit_shared_pm": lambda kern: lib.rti_fit_shared_pm(p, 6, 20, p, L.RTI_F32, 64, 1, 0, 0, p, 0, 0, kern,
+                                                                None),
+        "rti_fit_shared_q8": lambda kern: lib.rti_fit_shared_q8(p, 6, 20, p, 64, 1, 0, 0, p, 0, 0, kern, None),
+        "rti_fit_shared_h16": lambda kern: lib.rti_fit_shared_h16(p, 6, 20, p, 64, 1, 0, 0, p, 0, 0, kern, None),
+        "rti_fit_shared_residual": lambda kern: lib.rti_fit_shared_residual(p, p, 6, 20, p, L.RTI_F32, 64, 1, 0, 0, p,
+                                                                            0, 0, p, p, kern, None),
+        "rti_fit_shared_residual_svd": lambda kern: lib.rti_fit_shared_residual_svd(p, p, 6, 20, p, L.RTI_F32, 64, 1, 0,
+                                                                                    0, p, 0, 0, p, p, kern, None),
+    }
+    # the bits each entry documents (include/rti.h); every other single bit must be refused
+    chunks, planes = 0xF << L.RTI_KERNEL_CHUNKS_SHIFT, 0xF << L.RTI_KERNEL_TILE_PLANES_SHIFT
+    depth, waves = 0xF << L.RTI_KERNEL_TILE_DEPTH_SHIFT, 0xF << L.RTI_KERNEL_TILE_WAVES_SHIFT
+    allowed = {
+        "rti_fit_shared": 0xFF | L.RTI_KERNEL_NONTEMPORAL | L.RTI_KERNEL_PINV_LDS | L.RTI_KERNEL_NT_STORE
+        | L.RTI_KERNEL_STAGE | L.RTI_KERNEL_ROTATE | L.RTI_KERNEL_ROUNDS | L.RTI_KERNEL_ONE_LAUNCH | chunks | planes
+        | depth | waves,
+        "rti_fit_shared_pm": 0xFF | L.RTI_KERNEL_STAGE | L.RTI_KERNEL_NT_STORE | L.RTI_KERNEL_ROTATE | chunks | waves,
+        "rti_fit_shared_q8": L.RTI_KERNEL_STAGE | chunks | depth,
+        "rti_fit_shared_h16": chunks | depth | waves,
+        "rti_fit_shared_residual": L.RTI_KERNEL_ONE_LAUNCH | chunks,
+        "rti_fit_shared_residual_svd": L.RTI_KERNEL_ONE_LAUNCH | chunks,
+    }
+    for name, call in calls.items():
+        for bit in range(8, 32):
+            flag = ctypes.c_int(1 << bit).value
+            if allowed[name] & (1 << bit):
+                continue
+            assert call(flag) == L.RTI_ERR_BAD_ARG, (name, hex(1 << bit))
+            assert b"kernel bits" in lib.rti_last_error(), name
+        # selectors past the ones the entry documents
+        top = L.RTI_KERNEL_TILE if allowed[name] & 0xFF else L.RTI_KERNEL_AUTO
+        assert call(top + 1) == L.RTI_ERR_BAD_ARG, name
+    # the retired pixel-major measurement modes (r04: "no stores" / "no arithmetic" / SGPR weights)
+    for flag in (L.RTI_KERNEL_ONE_LAUNCH, L.RTI_KERNEL_ROUNDS, L.RTI_KERNEL_PINV_LDS):
+        assert calls["rti_fit_shared_pm"](flag) == L.RTI_ERR_BAD_ARG
+        assert lib.rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 64, 1, 0, 0, flag) == 0

@@ -148,3 +148,80 @@ def test_config4_4k_relight_1000_evals():
         rf = o.relight(coef[rows].cpu().numpy(), "ptm", lu[e], lv[e])[0]
         near = np.abs(rf - np.round(rf)) < 1e-3
         assert not ((i32 != np.trunc(rf)) & ~near).any(), e
+
+
+def _u8_checks(I8, lu, lv, basis, k, idx_per_c):
+    """AUTO on an 8-bit stack (the reference's V channel, analysis.py:219) runs the split-fp16 fit
+    (rti_fit_shared_h16): the whole map against the fp32 stream on the same values (fit_shared_into, the
+    kernel test_gpu_fit / test_config3 pin), sampled pixels against the fp64 oracle, and linearity."""
+    dev = I8.device
+    C, N, P = I8.shape
+    pinv64 = o.pinv_shared(basis, lu, lv) if basis == "ptm" else np.linalg.pinv(o.design("hsh", lu, lv))
+    coef = rti.fit(I8.reshape(C, N, 1, P), lu, lv, basis=basis).reshape(C, P, k)  # AUTO -> h16 for uint8
+    pv = torch.as_tensor(rti.pinv(lu, lv, basis).astype(np.float32), device=dev)
+    for c in range(C):
+        ref32 = rti.fit_shared_into(pv, I8[c].float(), torch.empty((P, k), device=dev), k=k, kernel="auto")
+        s = ref32.abs().amax(1, keepdim=True).clamp_min(1.0)
+        assert float(((coef[c] - ref32) / s).abs().max()) < 1e-5, c
+        del ref32
+        idx = idx_per_c[c]
+        check_sampled(coef[c][idx].cpu().numpy(), I8[c][:, idx].float().cpu().numpy(), pinv64)
+    return coef, pinv64
+
+
+def test_config2_4k_n100_u8_h16():
+    """configs[2] on the reference's own 8-bit intensities: 4K × 100 uint8 through rti.fit's AUTO (the h16
+    fit, 1024-pixel tiles two per CU): whole-map agreement with the fp32 stream, sampled fp64 parity
+    including the last pixels, and fit(2I + 3) = 2·fit(I) + 3·pinv·1 on I <= 126 (2I + 3 stays 8-bit)."""
+    dev = torch.device("cuda", 0)
+    H, W, N = 2160, 3840, 100
+    P = H * W
+    lu, lv = o.synth_dirs(N, 2)
+    g = torch.Generator(device=dev).manual_seed(21)
+    I8 = torch.randint(0, 127, (1, N, P), generator=g, device=dev, dtype=torch.uint8)
+    idx = torch.cat([torch.randint(0, P, (4096,), generator=g, device=dev), torch.arange(P - 2048, P, device=dev)])
+    coef, pinv64 = _u8_checks(I8, lu, lv, "ptm", 6, [idx])
+    coef2 = rti.fit((2 * I8 + 3).reshape(1, N, 1, P), lu, lv).reshape(1, P, 6)
+    c3 = torch.as_tensor(pinv64.sum(1) * 3, device=dev, dtype=torch.float32)
+    s2 = coef[0].abs().amax(1, keepdim=True).clamp_min(1.0)
+    assert float(((coef2[0] - 2 * coef[0] - c3) / (2 * s2)).abs().max()) < 1e-4
+
+
+def test_config3_4k_rgb_n200_u8_h16():
+    """configs[3] with 8-bit channels: 3 × 200 × 8.29 M = 4.98e9 bytes, past 2^32, through the h16 fit
+    (2048-pixel tiles, HSH-16): whole maps against the fp32 stream channel by channel, sampled fp64 parity
+    in every channel including the last pixels of the last channel (offsets past 2^32 bytes)."""
+    dev = torch.device("cuda", 0)
+    H, W, N, C = 2160, 3840, 200, 3
+    P = H * W
+    lu, lv = o.synth_dirs(N, 3)
+    g = torch.Generator(device=dev).manual_seed(33)
+    I8 = torch.randint(0, 256, (C, N, P), generator=g, device=dev, dtype=torch.uint8)
+    assert I8.numel() > 2 ** 32
+    idx = [torch.cat([torch.randint(0, P, (2048,), generator=g, device=dev), torch.arange(P - 1024, P, device=dev)])
+           for _ in range(C)]
+    _u8_checks(I8, lu, lv, "hsh", 16, idx)
+
+
+def test_config3_4k_rgb_n200_hsh16_pixel_major():
+    """configs[3] in the reference's pixel-major layout ([C][P][N], analysis.py:217-219): AUTO for k = 16 is
+    the direct form (rti_fit_shared_pm, stack loaded straight into MFMA operands).  Whole maps against the
+    light-major fit of the same values, sampled fp64 parity including the last pixels of the last channel."""
+    dev = torch.device("cuda", 0)
+    H, W, N, C = 2160, 3840, 200, 3
+    P = H * W
+    lu, lv = o.synth_dirs(N, 3)
+    pinv64 = np.linalg.pinv(o.design("hsh", lu, lv))
+    assert rti._lib.lib().rti_fit_shared_pm_plan(16, N, rti._lib.RTI_F32, P, C, 0, 0, 0) // 10 ** 8 == \
+        rti._lib.RTI_PM_DIRECT
+    g = torch.Generator(device=dev).manual_seed(41)
+    Ipm = torch.randint(0, 256, (C, P, N), generator=g, device=dev, dtype=torch.uint8).float()  # 19.9 GB
+    coef = rti.fit(Ipm.reshape(C, H, W, N), lu, lv, basis="hsh", stack="pixel").reshape(C, P, 16)
+    pv = torch.as_tensor(rti.pinv(lu, lv, "hsh").astype(np.float32), device=dev)
+    for c in range(C):
+        lm = rti.fit_shared_into(pv, Ipm[c].T.contiguous(), torch.empty((P, 16), device=dev), k=16)
+        s = lm.abs().amax(1, keepdim=True).clamp_min(1.0)
+        assert float(((coef[c] - lm) / s).abs().max()) < 1e-5, c
+        del lm
+        idx = torch.cat([torch.randint(0, P, (2048,), generator=g, device=dev), torch.arange(P - 1024, P, device=dev)])
+        check_sampled(coef[c][idx].cpu().numpy(), Ipm[c][idx].T.cpu().numpy(), pinv64)

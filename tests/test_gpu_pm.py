@@ -37,6 +37,16 @@ def test_golden_256x256_N20_pixel_major(cuda):
         got = got.cpu().numpy() if layout == "pixel" else got.T.cpu().numpy()
         err, ok = coef_close(got.reshape(256, 256, 6), d["coef"])
         assert ok, ("stage", layout, err)
+    # the plan AUTO ran when round 4's uncommitted edit faulted: the MFMA stream, 8 waves, 19-KiB
+    # rings, one-group units, interleaved; now reachable as RTI_KERNEL_MFMA, its DMAs bounded by descriptors
+    fl = L.RTI_KERNEL_MFMA | (8 << L.RTI_KERNEL_TILE_WAVES_SHIFT)
+    assert L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, fl) == \
+        L.RTI_PM_MFMA_STREAM * 10**8 + 19 * 1000 + 8
+    pv = torch.as_tensor(rti.pinv(d["lu"], d["lv"], "ptm").astype(np.float32), device=cuda)
+    got = rti.api.fit_shared_pm_into(pv, Ipm.reshape(-1, 20), torch.empty((256 * 256, 6), device=cuda), k=6,
+                                     kernel="mfma", flags=8 << L.RTI_KERNEL_TILE_WAVES_SHIFT)
+    err, ok = coef_close(got.cpu().numpy().reshape(256, 256, 6), d["coef"])
+    assert ok, ("mfma stream w8", err)
     # a light-major-shaped VIEW of the pixel-major stack goes to the same kernel without a copy
     view = Ipm.permute(2, 0, 1)
     assert not view.is_contiguous()
@@ -194,3 +204,68 @@ def test_pm_full_size_4k_n100(cuda):
     assert float(((coef - a_true).abs() / scale).max()) < 1e-4
     lm = rti.fit(Ipm.T.contiguous().reshape(N, H, W), lu, lv).reshape(P, 6)
     assert float(((coef - lm).abs() / scale).max()) < 1e-5
+
+
+@pytest.mark.parametrize("N", [17, 20, 36, 50, 100])
+def test_pm_generations_many_blocks_per_wave(cuda, N):
+    """The VALU generations form (AUTO, k <= 9) with several 64-pixel blocks parked per wave (a ragged pixel
+    count: a partial last block), two channels, both layouts, and 1, 3 or 7 launches per channel
+    (RTI_KERNEL_CHUNKS forces the extra generations; the 4K full-size test runs AUTO's own 4), units of 1, 2
+    and 4 blocks (N % 4), interleaved (AUTO) or one contiguous run per wave (RTI_KERNEL_ROTATE): every
+    coefficient bit-identical whatever the split (a pixel's arithmetic does not depend on it)."""
+    P, C = next(p for p in range(300_001, 300_005) if p * N % 4 == 0), 2  # (P·N % 4 == 0: the DMA forms)
+    lu, lv = o.synth_dirs(N, 13)
+    pinv64 = np.linalg.pinv(o.design("ptm", lu, lv))
+    pv = torch.as_tensor(rti.pinv(lu, lv, "ptm").astype(np.float32), device=cuda)
+    rng = np.random.default_rng(N)
+    I = rng.integers(0, 256, size=(C, P, N)).astype(np.float32)
+    Id = torch.as_tensor(I, device=cuda)
+    assert L.lib().rti_fit_shared_pm_plan(6, N, L.RTI_F32, P, C, 0, 0, 0) // 10**8 == L.RTI_PM_VALU_STREAM
+    ref = _ref(I, pinv64)
+    for layout in ("pixel", "planar"):
+        outs = []
+        for gens, contig in ((0, 0), (3, 0), (7, 0), (0, L.RTI_KERNEL_ROTATE), (5, L.RTI_KERNEL_ROTATE)):
+            coef = torch.full((C, P, 6) if layout == "pixel" else (C, 6, P), float("nan"), device=cuda)
+            rti.api.fit_shared_pm_into(pv, Id, coef, k=6, layout=layout,
+                                       flags=(gens << L.RTI_KERNEL_CHUNKS_SHIFT) | contig)
+            assert L.lib().rti_last_launch_count() == C * max(gens, 1), gens  # the generations form ran
+            outs.append(coef.cpu().numpy())
+        got = outs[0] if layout == "pixel" else np.moveaxis(outs[0], 1, 2)
+        for c in range(C):
+            err, ok = coef_close(got[c], ref[c])
+            assert ok, (layout, c, err)
+        assert all(np.array_equal(outs[0], x) for x in outs[1:]), layout
+
+
+def test_pm_broadcast_stack_and_routing(cuda):
+    """ADVICE r04: a broadcast (stride-0) pixel-major stack is materialised, not read as dense by the C ABI;
+    stack="auto" sends a pixel-major view to rti_fit_shared_pm only for fp32 / int32 stacks and the kernels
+    it takes, and an explicit stack="pixel" refuses the rest."""
+    H, W, N = 24, 40, 20
+    lu, lv = o.synth_dirs(N, 4)
+    pinv64 = np.linalg.pinv(o.design("ptm", lu, lv))
+    rng = np.random.default_rng(3)
+    one = torch.as_tensor(rng.integers(0, 256, size=(H, W, N)).astype(np.float32), device=cuda)
+    ref = _ref(one.reshape(1, -1, N).cpu().numpy(), pinv64)[0].reshape(H, W, 6)
+    rgb = one.unsqueeze(0).expand(3, H, W, N)  # three channels sharing one stack (channel stride 0)
+    assert rgb.stride(0) == 0
+    coef = rti.fit(rgb, lu, lv, stack="pixel").cpu().numpy()
+    for c in range(3):
+        err, ok = coef_close(coef[c], ref)
+        assert ok, (c, err)
+    row = one[0, 0].reshape(1, 1, N).expand(H, W, N)  # every pixel the same row (pixel strides 0)
+    coef = rti.fit(row, lu, lv, stack="pixel").cpu().numpy()
+    err, ok = coef_close(coef, np.broadcast_to(ref[0, 0], (H, W, 6)))
+    assert ok, err
+    assert rti.api._pixel_major_of(rgb.permute(0, 3, 1, 2)) is None  # never routed as a pm view
+    coef = rti.fit(rgb.permute(0, 3, 1, 2), lu, lv).cpu().numpy()  # auto: the light-major copy
+    for c in range(3):
+        assert coef_close(coef[c], ref)[1]
+    # 8-bit views keep the copy + h16 path; explicit pm with a kernel it does not take raises
+    u8 = one.to(torch.uint8)
+    coef = rti.fit(u8.permute(2, 0, 1), lu, lv).cpu().numpy()
+    assert coef_close(coef, ref, rtol=1e-4)[1]
+    with pytest.raises(NotImplementedError):
+        rti.fit(one, lu, lv, stack="pixel", kernel="h16")
+    with pytest.raises(NotImplementedError):
+        rti.fit(one, lu, lv, stack="pixel", nontemporal=True)

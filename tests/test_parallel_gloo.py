@@ -182,3 +182,60 @@ def test_bench_spawns_ranks_strong_scaling(gpus):
 def test_bench_weak_option():
     line = _bench_plan(["--gpus", "2", "--plan", "--weak"])
     assert line["scaling"] == "weak" and line["config"]["H_per_rank"] == 2160 and line["config"]["H"] == 4320
+
+
+def _channels_worker(rank, world, port, H, W, C, chunks, partition, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rti.parallel import gather_evals, local_to_global_row
+
+        full_ref = torch.arange(C * H * W * 6, dtype=torch.float32).reshape(C, H, W, 6)
+        if partition == "cyclic":
+            local = torch.cat([full_ref[:, a:b] for a, b in cyclic_rows(H, world, rank, chunks)], dim=1)
+        else:
+            r0, r1 = row_range(H, world, rank)
+            local = full_ref[:, r0:r1].clone()
+        origins = []
+
+        def produce(c0, c1):  # every channel's rows of the chunk, as one fit launch produces them
+            origins.append(local_to_global_row(H, world, rank, chunks, partition, c0))
+            return local[:, c0:c1].clone()
+
+        full = gather_rows_pipelined(produce, local.shape[1], H, (W, 6), torch.float32, torch.device("cpu"),
+                                     chunks=chunks, partition=partition, channels=C)
+        # the global row origin of every produced chunk: its first row's index in the whole image
+        want = [int(local[0, c0, 0, 0]) // (W * 6) for c0 in
+                ([j * (local.shape[1] // chunks) for j in range(chunks)] if partition == "cyclic" else
+                 [row_range(local.shape[1], min(chunks, local.shape[1]) or 1, j)[0]
+                  for j in range(max(1, min(chunks, local.shape[1])))])] if local.shape[1] else []
+        ok_origins = origins == want[:len(origins)]
+        # relit rows [E, h, W] -> whole [E, H, W] images
+        E = 3
+        img_ref = torch.arange(E * H * W, dtype=torch.float32).reshape(E, H, W)
+        r0, r1 = row_range(H, world, rank)
+        imgs = gather_evals(img_ref[:, r0:r1], H)
+        q.put((rank, bool(torch.equal(full, full_ref)), ok_origins, bool(torch.equal(imgs, img_ref))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("H,W,C,chunks,world,partition", [(16, 3, 3, 4, 2, "block"), (11, 2, 3, 3, 3, "block"),
+                                                          (12, 2, 3, 2, 3, "cyclic"), (16, 4, 2, 4, 2, "cyclic")])
+def test_gather_rows_pipelined_channels(H, W, C, chunks, world, partition):
+    """C > 1 (RGB / HSH-16 maps): each chunk's rows of every channel gathered into the
+    [C, H, W, k] map (even and ragged block partitions, block-cyclic in place); the global row origin a
+    per-pixel chunk needs (analysis.py:228); relit row blocks reassembled into whole images."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_channels_worker, args=(r, world, port, H, W, C, chunks, partition, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, ok_origins, ok_imgs in results:
+        assert ok and ok_origins and ok_imgs, (rank, ok, ok_origins, ok_imgs)

@@ -1,0 +1,63 @@
+// Measurement-only build of the pixel-major VALU generations fit (not part of librti): the library's own
+// kernel source is compiled here with its PROBE template argument, which the C ABI cannot reach.
+//   pm_probe_vgen(mode = 0): exactly rti_fit_shared_pm's AUTO form (k = 6, fp32, pixel-major coefficients);
+//   mode = 1: the same launches with the coefficient stores dropped (reads + arithmetic only);
+//   mode | 2: each wave one contiguous run of blocks instead of interleaved units.
+#include "../../smartphone-based-rti_amd/csrc/rti_fit_pm.hip"
+
+#include <cstdio>
+
+namespace rti {
+int fail(int status, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+  fputc('\n', stderr);
+  return status;
+}
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? RTI_OK : fail(RTI_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+int device_cus() {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return cus;
+}
+void note_launches(int) {}
+}  // namespace rti
+
+template <int PROBE, int IL>
+static int probe_t(const float* pinv, int N, const float* I, int64_t P, float* coef, int w, int gens,
+                   hipStream_t s) {
+  using namespace rti;
+  const VPlan pl = vgen_plan(6, N, 4, w);
+  if (!pl.W || N % 4) return RTI_ERR_UNSUPPORTED;
+  auto kern = fit_pm_vgen<6, float, RTI_COEF_PIXEL_MAJOR, 4, vgen_mb(6), IL, PROBE>;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)pl.lds) != hipSuccess)
+    return RTI_ERR_HIP;
+  const int64_t cus = device_cus();
+  const VGens g = vgen_split(P, 6, cus * pl.W, gens, 0);  // N % 4 == 0: one-block units
+  for (int64_t b = 0; b < g.nbc; b += g.per) {
+    const int64_t n = g.nbc - b < g.per ? g.nbc - b : g.per;
+    const int64_t wgs = (n + pl.W - 1) / pl.W;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(wgs < cus ? wgs : cus)), dim3(64 * pl.W), pl.lds, s, pinv, N, I, P,
+                       coef, 64 * b, n, pl.ring, 0);
+  }
+  return check_launch("pm_probe_vgen");
+}
+
+extern "C" int pm_probe_vgen(const float* pinv, int N, const float* I, int64_t P, float* coef, int w, int gens,
+                             int mode, void* stream) {
+  // mode bit 0: no stores; bit 1: each wave one contiguous run (else interleaved units, the library's AUTO)
+  hipStream_t s = (hipStream_t)stream;
+  switch (mode & 3) {
+    case 0: return probe_t<0, 1>(pinv, N, I, P, coef, w, gens, s);
+    case 1: return probe_t<1, 1>(pinv, N, I, P, coef, w, gens, s);
+    case 2: return probe_t<0, 0>(pinv, N, I, P, coef, w, gens, s);
+    default: return probe_t<1, 0>(pinv, N, I, P, coef, w, gens, s);
+  }
+}

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Pixel-major shared fit (rti_fit_shared_pm) variants next to the light-major AUTO fit of the same
-values, interleaved in ONE process (HIP events per launch, median of --rounds):
-streaming ring at W waves per workgroup ("mfma", AUTO's form) and the double-buffered block form
-("tile", G 16-pixel groups per block).
+values, interleaved in ONE process (HIP events per launch, median of --rounds): the VALU generations
+form (AUTO for k <= 9) at W waves per CU, forced generation counts and contiguous runs, the MFMA stream
+("mfma") and block form ("tile"), the direct form, and (tools/probe/libpm_probe.so, when built) the
+generations kernel with its stores dropped.
 
   python tools/sweep_pm.py --config c3|c4|c2 [--rounds 20] [--waves 2,3,4,6,8] [--blocks 1,2,4]
 """
@@ -29,6 +30,7 @@ def main():
     ap.add_argument("--waves", default="2,3,4,6,8")
     ap.add_argument("--blocks", default="1,2")
     ap.add_argument("--in-dtype", default="f32", choices=["f32", "i32"])
+    ap.add_argument("--gens", default="6,8,12", help="VALU generations: launches per channel forced (CHUNKS)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L = rti._lib
@@ -77,24 +79,37 @@ def main():
         fl = w << L.RTI_KERNEL_TILE_WAVES_SHIFT
         plan = L.lib().rti_fit_shared_pm_plan(k, N, rti.api._IN_DTYPES[I.dtype], P, C, N, P * N, fl)
         if plan // 100000000 == L.RTI_PM_VALU_STREAM:
-            variants.append((f"pm_valu_w{w}_ring{plan % 100000000 // 1000}K",
+            variants.append((f"pm_vgen_w{w}_ring{plan % 100000000 // 1000}K",
+                             lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
+    if k <= 9:  # more (smaller) launch generations than AUTO's
+        for g in [int(x) for x in args.gens.split(",") if x]:
+            fl = g << L.RTI_KERNEL_CHUNKS_SHIFT
+            variants.append((f"pm_vgen_gens{g}",
                              lambda fl=fl: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto", flags=fl)))
     variants.append(("pm_auto", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto")))
-    if k <= 9:  # the VALU stream's weights by scalar loads (SGPRs) instead of the LDS copy
-        variants.append(("pm_valu_sgpr_weights", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
-                                                                                 flags=L.RTI_KERNEL_PINV_LDS)))
-    if k <= 9:  # measurement variants of the VALU stream: no stores / no arithmetic
-        st = 0
-        variants.append(("pm_valu_nostores", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
-                                                                              flags=st | L.RTI_KERNEL_ONE_LAUNCH)))
-        variants.append(("pm_valu_noarith", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
-                                                                             flags=st | L.RTI_KERNEL_ROUNDS)))
+    if k <= 9:  # each wave one contiguous run of blocks instead of interleaved units
+        variants.append(("pm_vgen_contig", lambda: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="auto",
+                                                                            flags=L.RTI_KERNEL_ROTATE)))
+    probe = os.path.join(ROOT, "tools", "probe", "libpm_probe.so")
+    if k == 6 and C == 1 and N % 4 == 0 and I.dtype == torch.float32 and os.path.exists(probe):
+        # tools/probe/pm_probe.hip: the library's generation kernel built with its stores dropped
+        import ctypes
+        plib = ctypes.CDLL(probe)
+        vp = ctypes.c_void_p
+
+        def pr(mode):
+            st = plib.pm_probe_vgen(vp(pv.data_ptr()), N, vp(Ipm.data_ptr()), ctypes.c_int64(P), vp(coef.data_ptr()),
+                                    0, 0, mode, vp(torch.cuda.current_stream(dev).cuda_stream))
+            assert st == 0, st
+        variants.append(("probe_vgen_same", lambda: pr(0)))
+        variants.append(("probe_vgen_nostores", lambda: pr(1)))
+        variants.append(("probe_vgen_contig_nostores", lambda: pr(3)))
     agree = {}
     for name, fn in variants:
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        if name not in ("light_major_auto", "pm_valu_nostores", "pm_valu_noarith"):
+        if name not in ("light_major_auto", "probe_vgen_nostores", "probe_vgen_contig_nostores"):
             scale = ref.abs().amax(-1, keepdim=True).clamp_min(1e-30)
             agree[name] = float(((coef - ref).abs() / scale).max())
             coef.fill_(float("nan"))
