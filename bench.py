@@ -380,7 +380,8 @@ class FitWorkload(Workload):
                "coef_layout": self.args.layout, "kernel": self.u8_kernel or self.args.kernel,
                "intensity_dtype": self.args.in_dtype, "stack_layout": self.stack}
         if self.stack == "pixel":
-            form = {1: "valu stream (one pixel per lane, packed FMA)", 2: "mfma stream", 3: "mfma block"}
+            form = {1: "valu generations (one pixel per lane, packed FMA, coefficients parked until the launch's end)",
+                    2: "mfma stream", 3: "mfma block", 4: "direct (stack straight into MFMA operands)"}
             cfg["pm_plan"] = {"form": form.get(self.pm_plan // 100000000), "waves_per_cu": self.pm_plan % 1000,
                               "kib_ring_or_px_block": self.pm_plan % 100000000 // 1000} \
                 if self.pm_plan else "one lane per pixel"

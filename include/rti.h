@@ -339,13 +339,14 @@ int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp,
  * out: F64 / F32 / I32 / U8, layout RTI_OUT_PIXEL_MAJOR ([p][e], the reference's
  * [y][x][ly][lx]) or RTI_OUT_EVAL_MAJOR ([e][p], prepare_images_data's [ly][lx][y][x]).
  * status: device int the caller zeroes; set to RTI_ERR_SINGULAR when a pixel's system is
- * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 4089
- * (RTI_ERR_UNSUPPORTED above: the one-column Cholesky panel's LDS; panels narrow from 32 columns at
- * N <= 568 to 1 above 3408, and the solve slows as n³/NB).
+ * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 32768 (RTI_ERR_UNSUPPORTED
+ * above): the Cholesky's panels narrow from 32 columns at N <= 568 to 1 at N <= 4089 (the panel in LDS), and
+ * above 4089 only the 32×32 diagonal block stays in LDS while the panel is solved in place in the slot.
  * Device memory: the call allocates (stream-ordered, hipMallocAsync) and frees a workspace of
  * P·N·(8 + 8) bytes (weights + nodes) plus, for N > 256, one Cholesky slot of ≈ 4·(N+pad)² bytes (the packed
  * lower triangle) per workgroup on min(P, CUs) workgroups (≈ 3.3 GB at N = 1800, 6.7 GB at N = 2556, 17 GB at
- * N = 4089 on 256 CUs), or for 139 <= N <= 256 an fp64 fallback slot of 8·N·(N+1) bytes per CU (below: in LDS),
+ * N = 4089 on 256 CUs; above 4089 as many slots as 48 GiB holds, at least one), or for 139 <= N <= 256 an fp64
+ * fallback slot of 8·N·(N+1) bytes per CU (below: in LDS),
  * plus a P + 1 int list of the fallback's pixels; RTI_ERR_HIP if it cannot. */
 int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                      const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,

@@ -22,6 +22,10 @@
 //    still 256 contiguous bytes per 16 lanes.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include <atomic>
 #include <cstdint>
 #include <type_traits>
@@ -42,6 +46,28 @@ int device_cus() {
     cache[dev].store(n, std::memory_order_relaxed);
   }
   return n;
+}
+
+hipError_t reserve_lds(const void* kern, size_t bytes) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<const void*, int>, size_t>> done;  // (kernel, device) -> bytes reserved
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  const std::pair<const void*, int> key(kern, dev);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto& e : done)
+      if (e.first == key && e.second >= bytes) return hipSuccess;
+  }
+  const hipError_t st = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (st == hipSuccess) {
+    std::lock_guard<std::mutex> g(mu);
+    bool found = false;
+    for (auto& e : done)
+      if (e.first == key) e.second = std::max(e.second, bytes), found = true;
+    if (!found) done.emplace_back(key, bytes);
+  }
+  return st;
 }
 
 namespace {
@@ -513,7 +539,8 @@ fit_shared_tile(const float* __restrict__ pinv, int k, int N, const T* __restric
 // as the waves grow and the registers go to loads in flight instead.
 // AHEAD = 0: ONE LDS tile (half the LDS, so twice the tile width fits: 16 KiB runs per wave and
 // plane at RC = 16), the next step's loads in registers during the compute, two barriers per step.
-// STORE: 1 plain coefficient stores, 2 non-temporal (RTI_KERNEL_NT_STORE, measurement), 0 none (probe)
+// STORE: 1 plain coefficient stores, 2 non-temporal, 3 non-temporal through an LDS stage (whole 128-B lines,
+// pixel-major k = 16), 0 none (probe)
 template <int RC, int W, int AHEAD, typename T, int LAYOUT, bool NT, int STORE = 1>
 __global__ void __launch_bounds__(64 * W)
 fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restrict__ I, int64_t P, int64_t pb,
@@ -622,11 +649,42 @@ fit_shared_tile_w(const float* __restrict__ pinv, int k, int N, const T* __restr
     return;
   }
   auto st16 = [&](float* p, floatx4 v) {
-    if constexpr (STORE == 2)
+    if constexpr (STORE >= 2)
       __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
     else
       *reinterpret_cast<floatx4*>(p) = v;
   };
+  if constexpr (STORE == 3 && LAYOUT == RTI_COEF_PIXEL_MAJOR) {
+    // k = 16, non-temporal and STAGED: a lane's registers hold 16-B quarters of 64-B pixel rows four pixels
+    // apart, so direct stores write every 128-B line in two halves, and non-temporal halves reach HBM
+    // separately (WRITE_SIZE 1.32x the coefficient bytes, r04).  Each wave instead parks a 64-pixel group
+    // (4 KiB) in its own slice of the now free LDS tile (the last step ended on a barrier) and writes it back
+    // as four 1-KiB contiguous non-temporal stores: whole lines.  16-B chunk ch of the group (pixel ch / 4,
+    // coefficients 4(ch % 4) ..) sits at chunk ch ^ ((ch >> 4) & 15) of the slice: the 16 lanes of a pass
+    // touch 16 distinct bank groups on both the writes and the reads.
+    float* __restrict__ slice = tile + wave * 1024;
+    auto sw = [](int ch) { return ch ^ ((ch >> 4) & 15); };
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t g0 = t0 + pw + 64 * g;  // first pixel of the group
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        *reinterpret_cast<floatx4*>(slice + 4 * sw((4 * q + c) * 4 + r)) = acc[g][c];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = 64 * j + lane;
+        const floatx4 v = *reinterpret_cast<const floatx4*>(slice + 4 * sw(ch));
+        if (g0 + (ch >> 2) < pe) st16(dst + g0 * 16 + 4 * ch, v);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice is rewritten by the next group
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return;
+  }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int64_t px = t0 + pw + 64 * g + 4 * q;
@@ -1060,8 +1118,7 @@ int launch_tile_t(const FitArgs& a) {
   if (lds > 160 * 1024)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
   auto kern = fit_shared_tile<RC, SP, T, LAYOUT, NT>;
-  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+  if (lds > 65536 && reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
   dim3 grid(grid_1d(a.P, R), a.C);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, a.stream, a.pinv, a.k, a.N, static_cast<const T*>(a.I), a.P,
@@ -1085,8 +1142,7 @@ int launch_tile_w_t(const FitArgs& a) {
   if (lds > 160 * 1024)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
   auto kern = fit_shared_tile_w<RC, W, AHEAD, T, LAYOUT, NT, STORE>;
-  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+  if (lds > 65536 && reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
   const int64_t pe = a.pe ? a.pe : a.P;
   dim3 grid(grid_1d(pe - a.pb, R), a.C);
@@ -1099,9 +1155,13 @@ int launch_tile_w_t(const FitArgs& a) {
 template <int RC, int AHEAD, int W = 8>
 int launch_tile_w_l(const FitArgs& a) {
   if constexpr (RC == 16 && AHEAD == 0) {  // AUTO's kernel: non-temporal coefficient stores
-    if ((a.mode & VM_NTS) && a.nt)
-      return a.layout == RTI_COEF_PLANAR ? launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, true, 2>(a)
-                                         : launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PIXEL_MAJOR, true, 2>(a);
+    // pixel-major HSH-16 rows leave through the LDS stage as whole lines (c4 3.21 against 3.40 ms for the
+    // per-lane quarter rows, profiles/r05d_c4_nts_staged_sweep.log; WRITE_SIZE back to the coefficient bytes)
+    if ((a.mode & VM_NTS) && a.nt) {
+      if (a.layout == RTI_COEF_PLANAR) return launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, true, 2>(a);
+      return a.k == 16 ? launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PIXEL_MAJOR, true, 3>(a)
+                       : launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PIXEL_MAJOR, true, 2>(a);
+    }
   }
   if (a.layout == RTI_COEF_PLANAR)
     return a.nt ? launch_tile_w_t<RC, W, AHEAD, float, RTI_COEF_PLANAR, true>(a)
@@ -1126,8 +1186,7 @@ int launch_tile_s_t(const FitArgs& a) {
   if (lds > 160 * 1024)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
   auto kern = fit_shared_tile_s<RC, W, float, LAYOUT, NT>;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
+  if (reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
   const int64_t tpc = (a.P + R - 1) / R, ntot = tpc * a.C, cus = device_cus();
   const dim3 grid((unsigned)(ntot < cus ? ntot : cus));
@@ -1159,8 +1218,7 @@ int launch_tile_dma_t(const FitArgs& a) {
   if (lds > 160 * 1024)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared: LDS tile ring of %zu B (N=%d) exceeds 160 KiB", lds, a.N);
   auto kern = fit_shared_tile_dma<RC, SP, NB, LAYOUT, NT>;
-  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+  if (lds > 65536 && reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared: cannot reserve %zu B of LDS", lds);
   dim3 grid(grid_1d(a.P, R), a.C);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, a.stream, a.pinv, a.k, a.N, static_cast<const float*>(a.I), a.P,

@@ -237,8 +237,7 @@ int launch_h16_t(const unsigned char* op, int N, const unsigned char* I, int64_t
   // AUTO batches 4 groups per read/MFMA round (c2 u8 0.0379 against 0.0443 ms one group at a time, c3 / c4 u8
   // within 1 %: profiles/r04z_h16_batch_sweep_c*.log); RTI_KERNEL_TILE_DEPTH(1|8) for measurement
   auto kern = cb == 8 ? fit_h16<K, LAYOUT, R, STEP, 8> : cb == 1 ? fit_h16<K, LAYOUT, R, STEP, 1> : fit_h16<K, LAYOUT, R, STEP, 4>;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
+  if (reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_h16: cannot reserve %zu B of LDS", lds);
   const int64_t tiles = (P + R - 1) / R;
   const dim3 grid((unsigned)((tiles + tpw - 1) / tpw), C);

@@ -559,7 +559,21 @@ fit_pm_vgen(const float* __restrict__ pinv, int N, const T* __restrict__ I, int6
           n = n4;
         }
       }
-      for (; n < N; ++n) {  // N % 4 (or every light when the rows are not 16-byte aligned)
+      if constexpr (ALIGN == 2) {  // N % 4 == 2: 8-byte aligned rows, light pairs by ds_read_b64
+        typedef T tx2 __attribute__((ext_vector_type(2)));
+        const int n2 = N & ~1;
+#pragma unroll 2
+        for (; n < n2; n += 2) {
+          int a = a0 + n * (int)sizeof(T);
+          a -= a >= ring ? ring : 0;
+          const tx2 v = *reinterpret_cast<const tx2*>(rp + a);
+          const f2 x = {to_f(v[0]), to_f(v[1])};
+#pragma unroll
+          for (int i = 0; i < K; ++i)
+            acc[i] = x * *reinterpret_cast<const f2*>(lw + (n >> 2) * 4 * K + 4 * i + (n & 3)) + acc[i];
+        }
+      }
+      for (; n < N; ++n) {  // N % 4 (or every light when the rows are not 8-byte aligned)
         int a = a0 + n * (int)sizeof(T);
         a -= a >= ring ? ring : 0;
         const float x = to_f(*reinterpret_cast<const T*>(rp + a));
@@ -812,8 +826,7 @@ PmPlan pm_plan(int N, size_t es, int g_req, int w_req) {
 template <int G, int K, typename T, int LAYOUT, int ALIGN>
 int launch_dma_t(const PmArgs& a, const PmPlan& pl) {
   auto kern = fit_pm_dma<G, K, T, LAYOUT, ALIGN>;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)pl.lds) != hipSuccess)
+  if (reserve_lds(reinterpret_cast<const void*>(kern), pl.lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
   const int64_t nblk = (a.P + 16 * G - 1) / (16 * G), units = nblk * a.C;
   const int64_t wgs_needed = (units + pl.W - 1) / pl.W;
@@ -886,8 +899,7 @@ StreamPlan stream_plan(int N, size_t es, int w_req, int u_req) {
 template <int K, typename T, int LAYOUT, int ALIGN, int NCH>
 int launch_stream_t(const PmArgs& a, const StreamPlan& pl) {
   auto kern = fit_pm_stream<K, T, LAYOUT, ALIGN, NCH>;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)pl.lds) != hipSuccess)
+  if (reserve_lds(reinterpret_cast<const void*>(kern), pl.lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
   const int64_t cus = device_cus();
   int g = 16, nn = a.N;  // U = (16 / gcd(N, 16)) · unit: a whole number of KiB (4-byte values)
@@ -981,8 +993,7 @@ template <int K, typename T, int LAYOUT, int ALIGN>
 int launch_vgen_t(const PmArgs& a, const VPlan& pl, int g_req, bool contig) {
   constexpr int MB = vgen_mb(K);
   auto kern = contig ? fit_pm_vgen<K, T, LAYOUT, ALIGN, MB, 0> : fit_pm_vgen<K, T, LAYOUT, ALIGN, MB, 1>;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)pl.lds) != hipSuccess)
+  if (reserve_lds(reinterpret_cast<const void*>(kern), pl.lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
   const int64_t cus = device_cus();
   const int ulog = contig ? 0 : vgen_ulog(a.N);
@@ -1011,6 +1022,9 @@ int launch_vgen_k(const PmArgs& a, const VPlan& pl, int g_req, bool contig) {
   if (a.N % 4 == 0)
     return planar ? launch_vgen_t<K, T, RTI_COEF_PLANAR, 4>(a, pl, g_req, contig)
                   : launch_vgen_t<K, T, RTI_COEF_PIXEL_MAJOR, 4>(a, pl, g_req, contig);
+  if (a.N % 2 == 0)
+    return planar ? launch_vgen_t<K, T, RTI_COEF_PLANAR, 2>(a, pl, g_req, contig)
+                  : launch_vgen_t<K, T, RTI_COEF_PIXEL_MAJOR, 2>(a, pl, g_req, contig);
   return planar ? launch_vgen_t<K, T, RTI_COEF_PLANAR, 1>(a, pl, g_req, contig)
                 : launch_vgen_t<K, T, RTI_COEF_PIXEL_MAJOR, 1>(a, pl, g_req, contig);
 }
@@ -1045,8 +1059,7 @@ int launch_direct_t(const PmArgs& a, const DirectOpts& o) {
   if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR)
     if (o.nts) kern = fit_pm_direct<K, T, LAYOUT, NS, D, true>;
   const size_t lds = (size_t)4 * RPX * K * sizeof(float);  // 4 waves per workgroup
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
+  if (reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
   const int64_t per = (tr + o.gens - 1) / o.gens;
   int launches = 0;

@@ -249,8 +249,7 @@ template <int K, int LAYOUT>
 int launch_q8_t(const Q8Args& a) {
   const size_t lds = q8_lds_bytes(a.N);
   auto kern = a.stage ? fit_q8<K, LAYOUT, true> : fit_q8<K, LAYOUT, false>;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
+  if (reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_q8: cannot reserve %zu B of LDS", lds);
   const int64_t pe = a.pe ? a.pe : a.P;
   const int64_t tiles = (pe - a.pb + Q8_R - 1) / Q8_R;

@@ -16,6 +16,10 @@ int fail(int status, const char* fmt, ...);
 int check_launch(const char* what);
 // compute units of the current HIP device (cached per device; rti_fit.hip)
 int device_cus();
+// hipFuncSetAttribute(kern, MaxDynamicSharedMemorySize, bytes) once per (kernel, device) and size: the call costs
+// microseconds of host time, which every launch of a stream-ordered entry point would otherwise pay
+// (rti_fit.hip)
+hipError_t reserve_lds(const void* kern, size_t bytes);
 // records the kernel launches of the current C-ABI call (rti_last_launch_count)
 void note_launches(int n);
 

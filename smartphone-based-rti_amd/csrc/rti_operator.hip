@@ -377,7 +377,7 @@ int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int 
   auto k = vec ? apply_op_f16s<T, TO, true> : apply_op_f16s<T, TO, false>;
   if (vec && ps && atoi(ps)) k = apply_op_f16s<T, TO, true, false>;
   if (lds > 65536 &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+      reserve_lds(reinterpret_cast<const void*>(k), lds) !=
           hipSuccess)
     return fail(RTI_ERR_HIP, "rti_apply_operator_f16: cannot reserve %zu B of LDS", lds);
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, hi, lo, Kp, inv_s, E, N, static_cast<const T*>(I), P, ls, cs,
@@ -408,10 +408,8 @@ int launch(const float* opT, int E, int N, int64_t os, const void* I, int64_t P,
   const unsigned gy = (unsigned)std::max(1, std::min(ntiles, (int)((2048 + gx - 1) / gx)));
   dim3 grid(gx, gy, C);
   if (lds > 65536) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(apply_op_mfma<T, TO, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(apply_op_mfma<T, TO, false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)reserve_lds(reinterpret_cast<const void*>(apply_op_mfma<T, TO, true>), lds);
+    (void)reserve_lds(reinterpret_cast<const void*>(apply_op_mfma<T, TO, false>), lds);
   }
   if (vec)
     hipLaunchKernelGGL((apply_op_mfma<T, TO, true>), grid, dim3(256), lds, s, opT, E, N, os, static_cast<const T*>(I),

@@ -951,6 +951,11 @@ __host__ __device__ constexpr int64_t chol_matrix_doubles(int N) {
   return ((int64_t)chol_ld(N) * (chol_ld(N) + 1) / 2 + 31) / 32 * 32;
 }
 __host__ __device__ constexpr int64_t chol_slot_doubles(int N) { return chol_matrix_doubles(N) + 3 * chol_ld(N); }
+// GP form (N > RBF_CH_MAX_N): + y1, y2 and the nodes (two float rows) in the slot
+__host__ __device__ constexpr int64_t chol_slot_doubles_gp(int N) { return chol_slot_doubles(N) + 3 * chol_ld(N); }
+constexpr int RBF_CH_GP_NB = 32;  // GP panel width (only its diagonal block is in LDS)
+constexpr int RBF_GP_MAX_N = 32768;  // a 4.3 GB slot per workgroup (the grid shrinks to fit RBF_GP_WS_BYTES)
+constexpr size_t RBF_GP_WS_BYTES = (size_t)48 << 30;
 
 // Phase timer for tools/probe/chol_probe.hip (compiled in only there): per workgroup, the steady-clock
 // ticks spent in each phase, summed over its pixels (a barrier closes every phase).
@@ -971,7 +976,10 @@ __device__ unsigned long long rti_chol_prof[1024][16];
   } while (0)
 #endif
 
-template <int NB, typename T>
+// GP (N > RBF_CH_MAX_N, whose one-column panel no longer fits the LDS): the same algorithm with only the NB×NB
+// diagonal block in LDS; the panel rows below it are read and solved in place in the slot's packed L (they ARE
+// the panel), and the right-hand sides and nodes live in the slot too (chol_slot_doubles_gp).
+template <int NB, typename T, bool GP = false>
 __global__ void __launch_bounds__(RBF_CH_THREADS)
 rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
                double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status,
@@ -979,18 +987,22 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
   static_assert(NB <= 32, "a wave solves both right-hand sides of a diagonal block (2·NB lanes)");
   constexpr int TH = RBF_CH_THREADS, LDP = NB + 1;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* pan = smem;                                        // [N][LDP]
-  double* y1 = pan + (size_t)N * LDP;                        // c₁ -> L⁻¹c₁ -> S⁻¹c₁
-  double* y2 = y1 + N;                                       // m  -> L⁻¹m  -> S⁻¹m
-  float* xs = reinterpret_cast<float*>(y2 + N);
-  float* ys = xs + N;
-  __shared__ double red[TH / 64];
-  __shared__ int s_bad;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n = N - 1, ld = chol_ld(N);
-  double* M = ws + (int64_t)blockIdx.x * chol_slot_doubles(N);
+  double* M = ws + (int64_t)blockIdx.x * (GP ? chol_slot_doubles_gp(N) : chol_slot_doubles(N));
+  double* pan = smem;                                                       // [N][LDP] (GP: [NB][LDP])
+  double* y1 = GP ? M + chol_slot_doubles(N) : pan + (size_t)N * LDP;      // c₁ -> L⁻¹c₁ -> S⁻¹c₁
+  double* y2 = y1 + (GP ? ld : N);                                          // m  -> L⁻¹m  -> S⁻¹m
+  float* xs = reinterpret_cast<float*>(y2 + (GP ? ld : N));
+  float* ys = xs + (GP ? ld : N);
+  __shared__ double red[TH / 64];
+  __shared__ int s_bad;
   // the lower triangle in packed rows (row i at i(i+1)/2): 4·ld² bytes per slot
   auto at = [&](int i, int j) -> int64_t { return (int64_t)i * (i + 1) / 2 + j; };
+  // element (r, c) of the panel at column k0: LDS, or (GP, rows below the diagonal block) the slot's L in place
+  auto pan_at = [&](int k0, int r, int c) -> double& {
+    return GP && r >= NB ? M[at(k0 + r, k0 + c)] : pan[r * LDP + c];
+  };
   double* gv = M + chol_matrix_doubles(N);  // g = A u
   double* cv = gv + ld;               // c = H b
   double* mv = cv + ld;               // m = (HAH)[:n, n], μ at n
@@ -1086,10 +1098,11 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
 
     // ---- blocked Cholesky S = L Lᵀ, with the forward substitutions L y = [c₁ | m] panel by panel --------
     for (int k0 = 0; k0 < n && !s_bad; k0 += NB) {  // s_bad: block-uniform after each sync
+      auto PAN = [&](int r, int c) -> double& { return pan_at(k0, r, c); };
       const int kb = min(NB, n - k0), rows = n - k0;
       // stage the panel rows [k0, n), columns [k0, k0 + kb); a short last panel (kb < NB, then rows = kb) is
       // padded to NB rows and columns with the identity, so the diagonal block's code below runs unguarded
-      for (int idx = t; idx < max(rows, NB) * NB; idx += TH) {
+      for (int idx = t; idx < (GP ? NB : max(rows, NB)) * NB; idx += TH) {  // (GP: the rest is in place)
         const int r = idx / NB, c = idx - r * NB;
         double v = r == c && r >= kb ? 1.0 : 0.0;
         if (c < kb && c <= r && r < rows) v = M[at(k0 + r, k0 + c)];
@@ -1138,17 +1151,17 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         double x[NB];
 #pragma unroll
         for (int c = 0; c < NB; ++c) {  // (rows below the block exist only when kb = NB)
-          double s = pan[r * LDP + c];
+          double s = PAN(r, c);
 #pragma unroll
           for (int q = 0; q < c; ++q) s = fma(-x[q], pan[c * LDP + q], s);
           x[c] = s * pan[c * LDP + NB];
         }
 #pragma unroll
-        for (int c = 0; c < NB; ++c) pan[r * LDP + c] = x[c];
+        for (int c = 0; c < NB; ++c) PAN(r, c) = x[c];
       }
       __syncthreads();
       CH_MARK(6);
-      for (int idx = t; idx < rows * NB; idx += TH) {  // write L's panel back (for the backward substitution)
+      for (int idx = t; idx < (GP ? min(rows, NB) : rows) * NB; idx += TH) {  // L's panel back to the slot
         const int r = idx / NB, c = idx - r * NB;
         if (c < kb && c <= r) M[at(k0 + r, k0 + c)] = pan[r * LDP + c];
       }
@@ -1156,7 +1169,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         double s1 = y1[k0 + r], s2 = y2[k0 + r];
 #pragma unroll
         for (int q = 0; q < NB; ++q) {  // (kb = NB here, as above)
-          const double l = pan[r * LDP + q];
+          const double l = PAN(r, q);
           s1 = fma(-l, y1[k0 + q], s1);
           s2 = fma(-l, y2[k0 + q], s2);
         }
@@ -1190,9 +1203,9 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         for (int q = 0; q < kb; ++q) {
           double li[8], lj[4];
 #pragma unroll
-          for (int a = 0; a < 8; ++a) li[a] = pan[min(ri + 8 * a, rows - 1) * LDP + q];  // rows past n: clamped
+          for (int a = 0; a < 8; ++a) li[a] = PAN(min(ri + 8 * a, rows - 1), q);  // rows past n: clamped
 #pragma unroll
-          for (int b = 0; b < 4; ++b) lj[b] = pan[min(rj + 8 * b, rows - 1) * LDP + q];  // reads, masked below
+          for (int b = 0; b < 4; ++b) lj[b] = PAN(min(rj + 8 * b, rows - 1), q);  // reads, masked below
 #pragma unroll
           for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -1304,10 +1317,16 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
     const unsigned cg = (unsigned)(P < chol_grid ? P : chol_grid);
     auto go = [&](auto kern) {
       const size_t lds = chol_lds_bytes(N, chol_nb(N));
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds);
+      (void)reserve_lds(reinterpret_cast<const void*>(kern), lds);
       hipLaunchKernelGGL(kern, dim3(cg), dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
     };
+    if (N > RBF_CH_MAX_N) {  // the panel below the diagonal block solved in place in the slot
+      constexpr int NB = RBF_CH_GP_NB;
+      auto kern = rbf_solve_chol<NB, T, true>;
+      const size_t lds = (size_t)NB * (NB + 1) * sizeof(double);
+      hipLaunchKernelGGL(kern, dim3(cg), dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
+      return;
+    }
     switch (chol_nb(N)) {
       case 32: go(rbf_solve_chol<32, T>); break;
       case 16: go(rbf_solve_chol<16, T>); break;
@@ -1331,8 +1350,7 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
     const unsigned fg = (unsigned)(P < fb_grid ? P : fb_grid);
     if (fb_in_lds(N)) {
       const size_t mb = (size_t)N * (N + 1) * sizeof(double);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rbf_solve_fp64<T, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)mb);
+      (void)reserve_lds(reinterpret_cast<const void*>(rbf_solve_fp64<T, true>), mb);
       hipLaunchKernelGGL((rbf_solve_fp64<T, true>), dim3(fg), dim3(RBF_FB_THREADS), mb, s, lu, lv, In, N, P, redo,
                          fb_ws, wT, status, fallback_px);
     } else {
@@ -1388,8 +1406,8 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
                                    int* fallback_px, rti_stream_t stream) {
   if (!lu || !lv || !I || !luv || !out || !status) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: null pointer");
   if (N <= 0 || P <= 0 || E <= 0) return fail(RTI_ERR_BAD_ARG, "rti_rbf_perpixel: N, P, E must be positive");
-  if (N > RBF_CH_MAX_N)
-    return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: N=%d > %d lights", N, RBF_CH_MAX_N);
+  if (N > RBF_GP_MAX_N)
+    return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: N=%d > %d lights", N, RBF_GP_MAX_N);
   if (P > 0x7fffffff) return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: P too large for one launch");
   if (in_dtype != RTI_F32 && in_dtype != RTI_U8 && in_dtype != RTI_I32)
     return fail(RTI_ERR_UNSUPPORTED, "rti_rbf_perpixel: input dtype %d", in_dtype);
@@ -1405,10 +1423,15 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   // + for the block solvers: the fp64 fallback's pixel list and (N > RBF_FB_LDS_N) per-workgroup matrices
   const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
-  const int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
+  int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
+  const int64_t slot_doubles = N > RBF_CH_MAX_N ? chol_slot_doubles_gp(N) : chol_slot_doubles(N);
+  if (chol && N > RBF_CH_MAX_N) {  // GP slots (≈ 4·N² bytes each): as many workgroups as RBF_GP_WS_BYTES holds
+    const int64_t fit = (int64_t)(RBF_GP_WS_BYTES / ((size_t)slot_doubles * sizeof(double)));
+    chol_grid = fit < 1 ? 1 : (fit < chol_grid ? fit : chol_grid);
+  }
   const int64_t fb_grid = fb ? (P < device_cus() ? P : device_cus()) : 0;
   const size_t fb_ws_bytes = fb ? (fb_in_lds(N) ? 0 : (size_t)fb_grid * N * (N + 1) * sizeof(double))
-                                : (chol ? (size_t)chol_grid * chol_slot_doubles(N) * sizeof(double) : 0);
+                                : (chol ? (size_t)chol_grid * slot_doubles * sizeof(double) : 0);
   const size_t flag_bytes = fb ? ((size_t)(P + 1) * sizeof(int) + 255) / 256 * 256 : 0;  // count + pixel list
   const size_t bytes = (size_t)N * P * (sizeof(double) + sizeof(float2)) + fb_ws_bytes + flag_bytes;
   if (hipMallocAsync(&ws, bytes, s) != hipSuccess)

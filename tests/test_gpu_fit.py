@@ -317,6 +317,13 @@ def test_launch_generations_bit_identical(cuda, basis, N, C, layout):
     assert int(L.lib().rti_last_launch_count()) == 1
     torch.cuda.synchronize()
     assert torch.equal(r, b)
+    if k == 16:  # AUTO's non-temporal LDS-staged whole-line stores against the plain per-lane stores of TILE
+        s = torch.full(shape, float("nan"), device=cuda)
+        rti.fit_shared_into(pv, I, s, k=k, layout=layout, kernel="tile",
+                            flags=(15 << L.RTI_KERNEL_CHUNKS_SHIFT) | (1 << L.RTI_KERNEL_TILE_DEPTH_SHIFT)
+                            | (8 << L.RTI_KERNEL_TILE_WAVES_SHIFT) | L.RTI_KERNEL_NONTEMPORAL)
+        torch.cuda.synchronize()
+        assert torch.equal(s, b)
     # and against the fp64 oracle on sampled pixels of the last channel (parts' boundaries included)
     px = np.unique(np.concatenate([np.random.default_rng(5).integers(0, P, 512), [0, P - 1, P // 5, P // 5 - 1]]))
     ref = o.fit_shared(I[-1][:, torch.as_tensor(px, device=cuda)].cpu().numpy(), o.pinv_shared(basis, lu, lv))

@@ -193,16 +193,17 @@ def test_compat_default_interpolation_perpixel(cuda):
 
 
 @pytest.mark.parametrize("n", [2, 6, 37, 64, 65, 80, 81, 100, 127, 128, 129, 160, 200, 248, 249, 255, 256,
-                               257, 300, 400, 512, 568, 569, 1100, 1800, 2557, 3000, 3500])
+                               257, 300, 400, 512, 568, 569, 1100, 1800, 2557, 3000, 3500, 4089, 4090, 5000])
 def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     """Every solver of rti_rbf_perpixel: fp64 register Gauss-Jordan (N <= 80) and the register-blocked
     fp32 Gauss-Jordan inverse + fp64 refinement on the full 16x16 block grid (N <= 128), the
     lower-triangle block grid (N <= 248) and the full 32x32 grid (N <= 256) (SURVEY §6 timed the
     reference at N = 200), and above 256 lights the blocked fp64 Cholesky (panels of 32 lights to N = 568,
-    16 to 1022, 8 to 1704, 4 to 2556, 2 to 3408, 1 to 4089; the reference takes N = frames/8 with no cap,
+    16 to 1022, 8 to 1704, 4 to 2556, 2 to 3408, 1 to 4089; above that the same solver with only the diagonal
+    block in LDS and the panel solved in place in global memory — the reference takes N = frames/8 with no cap,
     analysis.py:120,152), each with the reference's per-pixel geometry, against SciPy's fp64 solve restated
-    in the oracle.  (N > 1800 runs on 4 pixels: each pixel is one workgroup's seconds of work; 3500 takes the
-    one-column panel.)"""
+    in the oracle.  (N > 1800 runs on 4 pixels: each pixel is one workgroup's seconds of work; 3500 and 4089
+    take the one-column panel, 4090 and 5000 the global-panel form.)"""
     ys, xs = np.mgrid[0:3, 0:5] if n <= 1800 else np.mgrid[0:2, 0:2]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
@@ -216,11 +217,11 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     assert ok, err
 
 
-@pytest.mark.parametrize("n", [81, 128, 129, 200, 256, 257, 400, 600])
+@pytest.mark.parametrize("n", [81, 128, 129, 200, 256, 257, 400, 600, 4100])
 def test_rbf_perpixel_large_n_repeated_node_raises(cuda, n):
     """A repeated light direction makes A exactly singular: SciPy raises LinAlgError; so do the
-    block Gauss-Jordan and the blocked Cholesky solvers; N above the one-column Cholesky panel's LDS
-    limit (4089 lights: a 17-minute capture at 30 fps) is refused (RTI_ERR_UNSUPPORTED)."""
+    block Gauss-Jordan and the blocked Cholesky solvers (LDS and global panels); N above 32768 lights
+    (a 2.4-hour capture at 30 fps: a 4.3 GB fp64 slot per workgroup) is refused (RTI_ERR_UNSUPPORTED)."""
     ys, xs = np.mgrid[0:2, 0:2]
     rng = np.random.default_rng(n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
@@ -231,8 +232,8 @@ def test_rbf_perpixel_large_n_repeated_node_raises(cuda, n):
     with pytest.raises(np.linalg.LinAlgError):
         rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv)
     with pytest.raises(NotImplementedError):
-        rti.interpolate_rbf_perpixel(torch.zeros((1, 4090), dtype=torch.int32, device=cuda),
-                                     np.zeros((1, 4090), np.float32), np.zeros((1, 4090), np.float32), qu, qv)
+        rti.interpolate_rbf_perpixel(torch.zeros((1, 32769), dtype=torch.int32, device=cuda),
+                                     np.zeros((1, 32769), np.float32), np.zeros((1, 32769), np.float32), qu, qv)
 
 
 @pytest.mark.parametrize("n", [100, 200, 256, 300])

@@ -25,7 +25,7 @@ for k in ${KEYS:-c3 c2 c4 c3u8 c4u8 c10 c6 c7 c5 c9}; do
     c10) run c10 "--config c10" fit_shared_residual_k 3550003200 8;;
     c6) run c6 "--config c6" fit_perpixel_cam 3516825600 1;;
     c7) run c7-split16 "--config c7" apply_op 6464000000 1;;
-    c3pm) run c3-auto-pixel-pm "--config c3 --stack pixel" fit_pm_vstream 3516825600 1;;
+    c3pm) run c3-auto-pixel-pm "--config c3 --stack pixel" fit_pm_vgen 3516825600 4;;
     c4pm) run c4-auto-pixel-pm "--config c4 --stack pixel" fit_pm_direct 21499084800 1;;
     c8n400) LAUNCHES=1 timeout -k 10 600 tools/pmc_pass.sh c8n400-chol "400" rbf_solve_chol 1792000000 \
               tools/sweep_chol.py > gpurun_out/pmc_c8n400-chol.log 2>&1

@@ -13,6 +13,9 @@
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I smartphone-based-rti_amd/csrc
 //        tools/probe/chol_probe.hip smartphone-based-rti_amd/csrc/rti_host.cpp -o tools/probe/chol_probe
 namespace rti {
+hipError_t reserve_lds(const void* kern, size_t bytes) {  // librti's (cached) lives in rti_fit.hip
+  return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
 int device_cus() {  // librti's lives in rti_fit.hip
   int cus = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);

@@ -4,6 +4,12 @@
 // helps the c7 table writes.
 #include "../../smartphone-based-rti_amd/csrc/rti_operator.hip"
 
+namespace rti {
+hipError_t reserve_lds(const void* kern, size_t bytes) {  // librti's (cached) lives in rti_fit.hip
+  return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+}  // namespace rti
+
 extern "C" int probe_op(const void* hi, const void* lo, int Kp, float inv_s, int E, int N, const float* I, int64_t P,
                         int64_t p0, int64_t np, int gy, int* out, void* stream) {
   const size_t lds = (size_t)2 * rti::TP16 * (Kp + 8) * sizeof(_Float16);

@@ -20,6 +20,9 @@ int check_launch(const char* what) {
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? RTI_OK : fail(RTI_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }
+hipError_t reserve_lds(const void* kern, size_t bytes) {  // librti's (cached) lives in rti_fit.hip
+  return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
 int device_cus() {
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
