@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--tpw", default="0")
+    ap.add_argument("--batches", default="1,4,8")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L = rti._lib
@@ -42,11 +43,16 @@ def main():
     variants = []
     for half in (1, 2):  # RTI_KERNEL_TILE_WAVES: 1 = 2048-pixel tiles (one workgroup per CU), 2 = 1024 (two)
         for tpw in [int(x) for x in args.tpw.split(",")]:
-            for cb in (1, 4, 8):  # groups batched per step (RTI_KERNEL_TILE_DEPTH)
+            for cb in [int(x) for x in args.batches.split(",") if x]:  # groups batched per step (TILE_DEPTH)
                 fl = (tpw << L.RTI_KERNEL_CHUNKS_SHIFT) | (cb << L.RTI_KERNEL_TILE_DEPTH_SHIFT) | \
                      (half << L.RTI_KERNEL_TILE_WAVES_SHIFT)
                 variants.append((f"h16_{'1024px' if half == 2 else '2048px'}_tpw{tpw or 'auto'}_batch{cb}",
                                  lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
+    # r05: AUTO's per-plane buffer loads (padded lights move no bytes) against the r04 flat loads that re-read
+    # plane N - 1 (RTI_KERNEL_TILE_PLANES(1), measurement)
+    variants.append(("h16_auto", lambda: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel")))
+    fl1 = 1 << L.RTI_KERNEL_TILE_PLANES_SHIFT
+    variants.append(("h16_auto_flat_r04", lambda: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl1)))
     rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
     same = {}
     for name, fn in variants:
