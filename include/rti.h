@@ -146,25 +146,29 @@ int rti_fit_shared(const float* pinv, int k, int N,
  *   coef[c][p][i] = Σ_n pinv[i][n] · I[c*channel_stride + p*pixel_stride + n]
  * (pixel_stride 0 = N, channel_stride 0 = P*pixel_stride).  pinv, coef, coef_layout and
  * coef_channel_stride as rti_fit_shared; in_dtype F32 / I32 / U8.
- * AUTO for k <= 9 streams runs of 16-pixel groups (contiguous 16·N values each) HBM -> a per-wave LDS ring by
- * 1-KiB LDS-DMAs and contracts them there, one pixel per lane with packed FMAs; for k = 16 (and with
- * RTI_KERNEL_STAGE for any k) the DIRECT form loads the groups straight into VGPRs as v_mfma_f32_16x16x4_f32
- * operands and writes the coefficients in LDS-staged bursts (N % 4 == 0, N <= 256).  RTI_KERNEL_MFMA: the
- * MFMA stream through the LDS ring for every k; RTI_KERNEL_TILE: a double-buffered block form.
+ * AUTO for k <= 9 (the VALU generations form): launches over a channel's 64-pixel blocks in which every wave
+ * streams its units HBM -> a private LDS ring by 1-KiB LDS-DMAs (bounded buffer loads), computes one pixel per
+ * lane with packed FMAs and keeps the coefficients in registers until the launch's end (one store burst per
+ * wave).  AUTO for k = 16, and with RTI_KERNEL_STAGE for any k: the DIRECT form loads 16-pixel groups straight
+ * into VGPRs as v_mfma_f32_16x16x4_f32 operands and writes the coefficients in LDS-staged 1-KiB bursts
+ * (non-temporal for AUTO k = 16; N % 4 == 0, N <= 256).  RTI_KERNEL_MFMA: the MFMA stream through the LDS ring
+ * for every k; RTI_KERNEL_TILE: a double-buffered block form.  All forms compute the same coefficients.
  * These take F32 / I32 stacks, k in {6, 9, 16}, pixel_stride = N, P·N and channel_stride multiples of 4,
- * I and coef 16-byte aligned, P·k·4 < 2^31 and N within the LDS budget (rti_fit_shared_pm_plan);
- * RTI_KERNEL_MFMA / TILE fail with RTI_ERR_UNSUPPORTED outside that, AUTO and RTI_KERNEL_VALU run one lane
- * per pixel instead (any shape, uint8 included).  Measurement flags: RTI_KERNEL_TILE_WAVES(W) waves per
- * workgroup (direct form: per CU), RTI_KERNEL_CHUNKS(n) (MFMA stream: n× the smallest unit; block form:
- * 16n-pixel blocks; direct form: n launch generations), RTI_KERNEL_ROTATE (MFMA stream: each wave one
- * contiguous run of units), RTI_KERNEL_PINV_LDS (VALU stream: the weights by scalar loads instead of its
- * LDS copy), RTI_KERNEL_ONE_LAUNCH / RTI_KERNEL_ROUNDS (VALU stream without stores / without arithmetic). */
+ * I 16-byte aligned, coef 8- (VALU generations) or 16-byte aligned, P·k·4 < 2^31 (all but the VALU
+ * generations) and N within the LDS budget (rti_fit_shared_pm_plan); RTI_KERNEL_MFMA / TILE fail with
+ * RTI_ERR_UNSUPPORTED outside that, AUTO and RTI_KERNEL_VALU run one lane per pixel instead (any shape, uint8
+ * included).  Tuning flags (the only bits accepted besides the selector; anything else is RTI_ERR_BAD_ARG):
+ * RTI_KERNEL_TILE_WAVES(W) waves per workgroup (direct form: per CU), RTI_KERNEL_CHUNKS(n) (VALU generations:
+ * at least n launches per channel; MFMA stream: n× the smallest unit; block form: 16n-pixel blocks; direct
+ * form: n launch generations), RTI_KERNEL_ROTATE (VALU generations and MFMA stream: each wave one contiguous
+ * run instead of interleaved units), RTI_KERNEL_NT_STORE (MFMA stream k = 16 and direct form: non-temporal
+ * coefficient stores), RTI_KERNEL_STAGE (AUTO: the direct form). */
 int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I, int in_dtype, int64_t P, int C,
                       int64_t pixel_stride, int64_t channel_stride,
                       float* coef, int coef_layout, int64_t coef_channel_stride,
                       int kernel, rti_stream_t stream);
 /* 0 if rti_fit_shared_pm runs one lane per pixel (the fallback) for this shape and kernel selection, else
- * form·10^8 + size·1000 + W: form RTI_PM_VALU_STREAM (AUTO, k <= 9: one pixel per lane, packed FMAs) or
+ * form·10^8 + size·1000 + W: form RTI_PM_VALU_STREAM (AUTO, k <= 9: the VALU generations form) or
  * RTI_PM_MFMA_STREAM (RTI_KERNEL_MFMA) with size = KiB of LDS ring per wave and W = waves per workgroup,
  * RTI_PM_BLOCK (RTI_KERNEL_TILE, or N too small for a ring) with size = pixels per block, or RTI_PM_DIRECT
  * (AUTO k = 16, AUTO | RTI_KERNEL_STAGE) with size = 16-light steps and W = waves per CU. */

@@ -91,12 +91,13 @@ constexpr int stores_per_group() {
   return 4;
 }
 
-template <int K, int LAYOUT>
+// AUX: the stores' cache policy (0 plain, 2 non-temporal)
+template <int K, int LAYOUT, int AUX = 0>
 __device__ __forceinline__ void store_group(__amdgpu_buffer_rsrc_t rs, floatx4 d, int64_t px, int64_t P, int r) {
   const bool pin = px < P;
   if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 4 == 0) {
     const uint32_t off = (pin && 4 * r < K) ? (uint32_t)((px * K + 4 * r) * 4) : PM_OOB;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(intx4, d), rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(intx4, d), rs, off, 0, AUX);
   } else if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR && K % 2 == 0) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -241,7 +242,9 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
 // NCH > 0: at most NCH 16-light chunks (N <= 16·NCH), fully unrolled with wave-uniform guards: the
 // operator's A fragments live in VGPRs (read once from LDS) and every chunk's B reads of a group are issued
 // before its first MFMA; NCH = 0: any N, one chunk per loop step with A from LDS.
-template <int K, typename T, int LAYOUT, int ALIGN, int NCH>
+// NTS: non-temporal coefficient stores (pixel-major k = 16: each group's 16 pixel rows are one 1-KiB line-aligned
+// store, AUTO for HSH-16)
+template <int K, typename T, int LAYOUT, int ALIGN, int NCH, bool NTS = false>
 __global__ void __launch_bounds__(512)
 fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
               float* __restrict__ coef, int64_t ocstride, int C, int U, int nu, int64_t tu, int ring, int contig) {
@@ -385,7 +388,7 @@ fit_pm_stream(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
       }
     }
     const floatx4 d = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    store_group<K, LAYOUT>(rs, d, px0 + q, P, r);  // groups past P: every store dropped
+    store_group<K, LAYOUT, NTS ? 2 : 0>(rs, d, px0 + q, P, r);  // groups past P: every store dropped
     // refill every KiB the groups 0..j freed
     const int lim0 = (end + ring) >> 10;
     const int lim = lim0 < dt ? lim0 : dt;
@@ -875,6 +878,7 @@ int launch_dma(const PmArgs& a, const PmPlan& pl) {
 // with 76-KiB rings; c4 4K RGB×200: 8 waves 3.80 ms, 4 waves 4.15-4.63; profiles/r04_pm_sweep.log)
 struct StreamPlan {
   int W = 0, ring = 0, contig = 0, unit = 1;
+  bool nts = false;  // non-temporal coefficient stores (k = 16, pixel-major)
   size_t lds = 0;
 };
 
@@ -899,6 +903,8 @@ StreamPlan stream_plan(int N, size_t es, int w_req, int u_req) {
 template <int K, typename T, int LAYOUT, int ALIGN, int NCH>
 int launch_stream_t(const PmArgs& a, const StreamPlan& pl) {
   auto kern = fit_pm_stream<K, T, LAYOUT, ALIGN, NCH>;
+  if constexpr (K == 16 && LAYOUT == RTI_COEF_PIXEL_MAJOR)
+    if (pl.nts) kern = fit_pm_stream<K, T, LAYOUT, ALIGN, NCH, true>;
   if (reserve_lds(reinterpret_cast<const void*>(kern), pl.lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_pm: LDS attribute");
   const int64_t cus = device_cus();
@@ -1236,17 +1242,21 @@ extern "C" int rti_fit_shared_pm(const float* pinv, int k, int N, const void* I,
       st = i32 ? launch_vgen<int32_t>(a, vp, c_req, contig) : launch_vgen<float>(a, vp, c_req, contig);
       break;
     }
-    case RTI_PM_DIRECT: {  // AUTO k = 16, AUTO | STAGE: straight to registers.  Measurement flags:
+    case RTI_PM_DIRECT: {  // AUTO k = 16, AUTO | STAGE: straight to registers.  Tuning flags:
       DirectOpts o;        // TILE_WAVES(w) waves per CU, CHUNKS(n) launch generations, NT_STORE non-temporal bursts
       if (w_req) o.wpc = w_req;
       if (c_req) o.gens = c_req;
-      o.nts = (kernel & RTI_KERNEL_NT_STORE) != 0;
+      // AUTO k = 16: the bursts non-temporal (whole 1-KiB lines; c4 3.677–3.696 against 3.731–3.745 ms plain,
+      // profiles/r05h_pm_sweep_c4.log, r05g); the MFMA stream ran 3.49–3.71 ms interleaved with other kernels
+      // but 4.13 ms back to back in bench.py (profiles/r05i_*), so it stays RTI_KERNEL_MFMA
+      o.nts = (kernel & RTI_KERNEL_NT_STORE) != 0 || (k == 16 && sel == RTI_KERNEL_AUTO && !(kernel & RTI_KERNEL_STAGE));
       st = i32 ? launch_direct<int32_t>(a, o) : launch_direct<float>(a, o);
       break;
     }
     case RTI_PM_MFMA_STREAM: {  // RTI_KERNEL_MFMA: the MFMA stream through the LDS ring
       StreamPlan sp = stream_plan(N, 4, w_req, c_req);
       sp.contig = (kernel & RTI_KERNEL_ROTATE) != 0;  // each wave one contiguous run of units
+      sp.nts = (kernel & RTI_KERNEL_NT_STORE) != 0;
       st = i32 ? launch_stream<int32_t>(a, sp) : launch_stream<float>(a, sp);
       break;
     }

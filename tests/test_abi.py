@@ -260,7 +260,7 @@ def test_entry_points_refuse_unknown_kernel_bits():
         | depth | waves,
         "rti_fit_shared_pm": 0xFF | L.RTI_KERNEL_STAGE | L.RTI_KERNEL_NT_STORE | L.RTI_KERNEL_ROTATE | chunks | waves,
         "rti_fit_shared_q8": L.RTI_KERNEL_STAGE | chunks | depth,
-        "rti_fit_shared_h16": chunks | depth | waves | planes,
+        "rti_fit_shared_h16": chunks | depth | waves,
         "rti_fit_shared_residual": L.RTI_KERNEL_ONE_LAUNCH | chunks,
         "rti_fit_shared_residual_svd": L.RTI_KERNEL_ONE_LAUNCH | chunks,
     }

@@ -205,8 +205,9 @@ def test_config3_4k_rgb_n200_u8_h16():
 
 def test_config3_4k_rgb_n200_hsh16_pixel_major():
     """configs[3] in the reference's pixel-major layout ([C][P][N], analysis.py:217-219): AUTO for k = 16 is
-    the direct form (rti_fit_shared_pm, stack loaded straight into MFMA operands).  Whole maps against the
-    light-major fit of the same values, sampled fp64 parity including the last pixels of the last channel."""
+    the direct form (rti_fit_shared_pm: the stack straight into v_mfma_f32_16x16x4_f32 operands, non-temporal
+    coefficient bursts); the MFMA stream (bounded LDS-DMA ring) runs too.  Whole maps against the light-major
+    fit of the same values, sampled fp64 parity including the last pixels of the last channel."""
     dev = torch.device("cuda", 0)
     H, W, N, C = 2160, 3840, 200, 3
     P = H * W
@@ -218,6 +219,10 @@ def test_config3_4k_rgb_n200_hsh16_pixel_major():
     Ipm = torch.randint(0, 256, (C, P, N), generator=g, device=dev, dtype=torch.uint8).float()  # 19.9 GB
     coef = rti.fit(Ipm.reshape(C, H, W, N), lu, lv, basis="hsh", stack="pixel").reshape(C, P, 16)
     pv = torch.as_tensor(rti.pinv(lu, lv, "hsh").astype(np.float32), device=dev)
+    direct = rti.api.fit_shared_pm_into(pv, Ipm, torch.empty((C, P, 16), device=dev), k=16, kernel="mfma")
+    s = coef.abs().amax(-1, keepdim=True).clamp_min(1.0)
+    assert float(((direct - coef) / s).abs().max()) < 1e-5
+    del direct
     for c in range(C):
         lm = rti.fit_shared_into(pv, Ipm[c].T.contiguous(), torch.empty((P, 16), device=dev), k=16)
         s = lm.abs().amax(1, keepdim=True).clamp_min(1.0)

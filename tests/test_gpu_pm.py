@@ -22,9 +22,9 @@ def test_golden_256x256_N20_pixel_major(cuda):
     plan = L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, 0)
     assert plan // 10**8 == L.RTI_PM_VALU_STREAM, plan  # AUTO for PTM-6: the packed-FMA stream
     plan = L.lib().rti_fit_shared_pm_plan(6, 20, L.RTI_F32, 256 * 256, 1, 0, 0, L.RTI_KERNEL_STAGE)
-    assert plan // 10**8 == L.RTI_PM_DIRECT, plan  # AUTO | STAGE: straight to registers (AUTO for HSH-16)
+    assert plan // 10**8 == L.RTI_PM_DIRECT, plan  # AUTO | STAGE: straight to registers
     plan = L.lib().rti_fit_shared_pm_plan(16, 20, L.RTI_F32, 256 * 256, 1, 0, 0, 0)
-    assert plan // 10**8 == L.RTI_PM_DIRECT, plan
+    assert plan // 10**8 == L.RTI_PM_DIRECT, plan  # AUTO for HSH-16: the direct form (non-temporal bursts)
     for layout in ("pixel", "planar"):
         coef = rti.fit(Ipm, d["lu"], d["lv"], stack="pixel", layout=layout).cpu().numpy()
         if layout == "planar":

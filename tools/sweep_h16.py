@@ -48,18 +48,26 @@ def main():
                      (half << L.RTI_KERNEL_TILE_WAVES_SHIFT)
                 variants.append((f"h16_{'1024px' if half == 2 else '2048px'}_tpw{tpw or 'auto'}_batch{cb}",
                                  lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
-    # r05: AUTO's per-plane buffer loads (padded lights move no bytes) against the r04 flat loads that re-read
-    # plane N - 1 (RTI_KERNEL_TILE_PLANES(1), measurement)
-    variants.append(("h16_auto", lambda: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel")))
-    fl1 = 1 << L.RTI_KERNEL_TILE_PLANES_SHIFT
-    variants.append(("h16_auto_flat_r04", lambda: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl1)))
+    probe = os.path.join(ROOT, "tools", "probe", "libh16_probe.so")
+    if C == 1 and os.path.exists(probe):  # tools/probe/h16_probe.hip: the library kernel with its stores dropped
+        import ctypes
+        plib = ctypes.CDLL(probe)
+        vp = ctypes.c_void_p
+
+        def pr(mode):
+            st = plib.h16_probe(vp(op.data_ptr()), k, N, vp(I8.data_ptr()), ctypes.c_int64(P), vp(coef.data_ptr()),
+                                mode, vp(torch.cuda.current_stream(dev).cuda_stream))
+            assert st == 0, st
+        variants.append(("probe_h16_same", lambda: pr(0)))
+        variants.append(("probe_h16_nostores", lambda: pr(1)))
+        variants.append(("probe_h16_nt_stores", lambda: pr(2)))
     rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
     same = {}
     for name, fn in variants:
         coef.fill_(float("nan"))
         fn()
         torch.cuda.synchronize()
-        same[name] = bool(torch.equal(coef, ref))
+        same[name] = bool(torch.equal(coef, ref)) if name != "probe_h16_nostores" else None
     stream = torch.cuda.current_stream(dev)
     times = {name: [] for name, _ in variants}
     for _ in range(args.rounds):

@@ -57,6 +57,9 @@ def main():
                 flu = fl | (u << L.RTI_KERNEL_CHUNKS_SHIFT)
                 variants.append((f"pm_stream_w{w}_unit{u}",
                                  lambda flu=flu: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="mfma", flags=flu)))
+            fln = fl | L.RTI_KERNEL_NT_STORE
+            variants.append((f"pm_stream_w{w}_nts",
+                             lambda fln=fln: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="mfma", flags=fln)))
             flc = fl | L.RTI_KERNEL_ROTATE
             variants.append((f"pm_stream_w{w}_contiguous",
                              lambda flc=flc: rti.api.fit_shared_pm_into(pv, Ipm, coef, k=k, kernel="mfma", flags=flc)))
