@@ -99,7 +99,8 @@ __device__ __forceinline__ void h16_store(float* __restrict__ dst, int64_t P, in
 
 // CB: 16-pixel groups whose reads and MFMAs are batched per step (AUTO 4; 1 one group at a time)
 // PROBE (not reachable from the C ABI; tools/probe/h16_probe.hip): 1 = the coefficient stores dropped, 2 = the
-// stores non-temporal
+// stores non-temporal, 3 / 4 = (PTM-6, 1024-pixel tiles) each wave's 128 finished pixel rows staged in the free
+// half of the LDS tile and written back as three whole 1-KiB stores, plain / non-temporal
 template <int K, int LAYOUT, int R, int STEP, int CB = 1, int PROBE = 0>
 __global__ void __launch_bounds__(64 * H16_W)
 fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __restrict__ I, int64_t pb, int64_t pe,
@@ -216,6 +217,45 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
     }
     zero();
   };
+  // staged form (PROBE 3 / 4): the wave's 128 rows of 6 coefficients (3 KiB) parked in its slice of the free tile
+  // buffer fb, read back as 16-B chunks 16·lane + 1 KiB·j and written as whole lines; the caller's barrier keeps
+  // the other waves from parking into fb before every wave has read its slice back
+  constexpr bool STG = (PROBE == 3 || PROBE == 4) && K == 6 && R == 1024 && LAYOUT == RTI_COEF_PIXEL_MAJOR;
+  auto finish_staged = [&](int ti, int fb) {
+    const int64_t w0 = tile_px(ti) + TL::WPX * wave;  // the wave's first pixel (1-KiB aligned rows)
+    float* slice = reinterpret_cast<float*>(tile + fb * (STEP * TL::RS)) + wave * (TL::WPX * 6);
+    if (g < 2) {
+      float sc[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sc[r] = inv_s[(4 * g + r) & 7];
+#pragma unroll
+      for (int c = 0; c < TL::G; ++c) {
+        float* row = slice + (16 * c + (lane & 15)) * 6 + 4 * g;
+        *reinterpret_cast<floatx2*>(row) = floatx2{acc[c][0] * sc[0], acc[c][1] * sc[1]};
+        if (g == 0) *reinterpret_cast<floatx2*>(row + 2) = floatx2{acc[c][2] * sc[2], acc[c][3] * sc[3]};
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int f = 256 * j + 4 * lane;  // the lane's first float of the wave's 768
+      const floatx4 v = *reinterpret_cast<const floatx4*>(slice + f);
+      float* d = dst + w0 * 6 + f;
+      if (w0 + (f + 3) / 6 < pe) {
+        if constexpr (PROBE == 4)
+          __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(d));
+        else
+          *reinterpret_cast<floatx4*>(d) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (w0 + (f + e) / 6 < pe) d[e] = v[e];
+      }
+    }
+    zero();
+  };
   // The stream loop of the q8 form: every vector-memory operation unconditional or in a fixed place (exact
   // counted vmcnt waits), loads of steps past the end re-read step S − 1, an odd stream gets one dummy step,
   // a finished tile's stores are issued at the start of the next step, before that step's loads; sb holds
@@ -227,18 +267,35 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
   __syncthreads();
   const int S2 = S + (S & 1);
   for (int s = 0; s < S2; s += 2) {
-    if (s > 0 && s % T == 0) finish(s / T - 1);
+    if (s > 0 && s % T == 0) {
+      if constexpr (STG) {  // buffer 1 is free here (its step was computed before the last barrier)
+        finish_staged(s / T - 1, 1);
+        __syncthreads();
+      } else {
+        finish(s / T - 1);
+      }
+    }
     load(min(s + 2, S - 1), sa);
     compute(0, s % T);
     park(1, sb);
     __syncthreads();
-    if (s + 1 < S && (s + 1) % T == 0) finish((s + 1) / T - 1);
+    if (s + 1 < S && (s + 1) % T == 0) {
+      if constexpr (STG) {  // buffer 0 is free here
+        finish_staged((s + 1) / T - 1, 0);
+        __syncthreads();
+      } else {
+        finish((s + 1) / T - 1);
+      }
+    }
     load(min(s + 3, S - 1), sb);
     if (s + 1 < S) compute(1, (s + 1) % T);
     park(0, sa);
     __syncthreads();
   }
-  finish(ntiles - 1);
+  if constexpr (STG)
+    finish_staged(ntiles - 1, 0);
+  else
+    finish(ntiles - 1);
 }
 
 template <int K, int LAYOUT, int R, int STEP>

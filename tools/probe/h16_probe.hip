@@ -2,7 +2,7 @@
 // launcher compiled with the PROBE template argument, which the C ABI cannot reach.
 //   h16_probe(mode = 0): exactly rti_fit_shared_h16's AUTO launch (1024-pixel tiles for k <= 9);
 //   mode = 1: the same launch with the coefficient stores dropped (reads + arithmetic only);
-//   mode = 2: the stores non-temporal.
+//   mode = 2: the stores non-temporal;  mode = 3 / 4 (k = 6): the rows staged through LDS, whole-line plain / NT stores.
 #include "../../smartphone-based-rti_amd/csrc/rti_fit_h16.hip"
 
 #include <cstdio>
@@ -50,9 +50,13 @@ extern "C" int h16_probe(const void* op, int k, int N, const void* I, int64_t P,
   const auto* o = static_cast<const unsigned char*>(op);
   const auto* x = static_cast<const unsigned char*>(I);
   hipStream_t s = (hipStream_t)stream;
-  if (k == 6)
-    return mode == 1 ? probe_t<6, 1>(o, N, x, P, coef, s) : mode == 2 ? probe_t<6, 2>(o, N, x, P, coef, s)
-                                                          : probe_t<6, 0>(o, N, x, P, coef, s);
+  if (k == 6) switch (mode) {
+      case 1: return probe_t<6, 1>(o, N, x, P, coef, s);
+      case 2: return probe_t<6, 2>(o, N, x, P, coef, s);
+      case 3: return probe_t<6, 3>(o, N, x, P, coef, s);
+      case 4: return probe_t<6, 4>(o, N, x, P, coef, s);
+      default: return probe_t<6, 0>(o, N, x, P, coef, s);
+    }
   if (k == 16)
     return mode == 1 ? probe_t<16, 1>(o, N, x, P, coef, s) : mode == 2 ? probe_t<16, 2>(o, N, x, P, coef, s)
                                                            : probe_t<16, 0>(o, N, x, P, coef, s);

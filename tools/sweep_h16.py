@@ -61,6 +61,9 @@ def main():
         variants.append(("probe_h16_same", lambda: pr(0)))
         variants.append(("probe_h16_nostores", lambda: pr(1)))
         variants.append(("probe_h16_nt_stores", lambda: pr(2)))
+        if k == 6:
+            variants.append(("probe_h16_staged", lambda: pr(3)))
+            variants.append(("probe_h16_staged_nt", lambda: pr(4)))
     rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
     same = {}
     for name, fn in variants:
