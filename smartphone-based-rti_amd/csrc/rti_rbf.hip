@@ -1110,34 +1110,33 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       }
       __syncthreads();
       CH_MARK(4);
-      if (wave == 0 && lane < NB) {  // the diagonal block in place in LDS, lane r updating row r (right-looking):
-        // the pivot and column c of L are uniform-address (broadcast) reads, the pivot's inverse square root is
-        // the fp64 rsq with two Newton steps (no sqrt / divide chains on this serial path); 1 / L[c][c] goes to
-        // the pitch column for the solves
-        double* row = pan + lane * LDP;
+      if (wave == 0 && lane < NB) {  // the diagonal block, lane r updating row r (right-looking), IN REGISTERS (r05):
+        // lane r holds its row a[0..NB) for the whole factorization; step c's pivot is lane c's a[c] and column c
+        // of L reaches every lane by readlane (no LDS round trip, fence or wave barrier per step: r04's form
+        // spent ≈ 220 µs per pixel at N = 400 on those).  The pivot's inverse square root is the fp64 rsq with
+        // two Newton steps; the arithmetic is r04's operation for operation (bit-identical L); the block and the
+        // reciprocals 1 / L[c][c] (pitch column) go back to LDS once, for the solves
+        double a[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) a[q] = pan[lane * LDP + q];
+        double rinv = 0.0;
         bool bad = false;
 #pragma unroll
         for (int c = 0; c < NB; ++c) {
-          const double d = pan[c * LDP + c];
+          const double d = readlane64(a[c], c);
           bad = bad || !(d > 0.0);
           double inv = __builtin_amdgcn_rsq(d);
           inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
           inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
-          if (lane == c) row[NB] = inv;
-          const double lrc = lane == c ? d * inv : row[c] * inv;  // L[r][c] (rows r >= c are used)
-          if (lane >= c) row[c] = lrc;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          double lq[NB];
+          if (lane == c) rinv = inv;
+          const double lrc = lane == c ? d * inv : a[c] * inv;  // L[r][c] (rows r >= c are used)
+          if (lane >= c) a[c] = lrc;
 #pragma unroll
-          for (int q = c + 1; q < NB; ++q) lq[q] = pan[q * LDP + c];
-#pragma unroll
-          for (int q = c + 1; q < NB; ++q) row[q] = fma(-lrc, lq[q], row[q]);  // L[r][q] −= L[r][c]·L[q][c]
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          for (int q = c + 1; q < NB; ++q) a[q] = fma(-lrc, readlane64(a[c], q), a[q]);  // −= L[r][c]·L[q][c]
         }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) pan[lane * LDP + q] = a[q];
+        pan[lane * LDP + NB] = rinv;
         if (bad && lane == 0) s_bad = 1;
       }
       __syncthreads();
