@@ -55,6 +55,7 @@ __device__ __forceinline__ double dist_eval(double qu, double qv, double xj, dou
 }
 
 
+typedef double dx4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ double readlane64(double x, int l) {
   const uint64_t u = __double_as_longlong(x);
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
@@ -979,13 +980,14 @@ __device__ unsigned long long rti_chol_prof[1024][16];
 // GP (N > RBF_CH_MAX_N, whose one-column panel no longer fits the LDS): the same algorithm with only the NB×NB
 // diagonal block in LDS; the panel rows below it are read and solved in place in the slot's packed L (they ARE
 // the panel), and the right-hand sides and nodes live in the slot too (chol_slot_doubles_gp).
-template <int NB, typename T, bool GP = false>
-__global__ void __launch_bounds__(RBF_CH_THREADS)
+// TH: threads per workgroup (AUTO 512, one workgroup per CU; 256 = two per CU, measurement: RTI_RBF_CHOL_TH)
+template <int NB, typename T, bool GP = false, int TH = RBF_CH_THREADS>
+__global__ void __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(TH == 256 ? 2 : 1)))
 rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
                double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status,
                double* __restrict__ ws) {
   static_assert(NB <= 32, "a wave solves both right-hand sides of a diagonal block (2·NB lanes)");
-  constexpr int TH = RBF_CH_THREADS, LDP = NB + 1;
+  constexpr int LDP = NB + 1;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n = N - 1, ld = chol_ld(N);
@@ -1181,42 +1183,98 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       // 12 reads per 32 fp64 FMAs
       const int m = rows - kb, T64 = (m + 63) / 64, nst = T64 * (T64 + 1);  // row tile I: 2I + 2 col tiles
       const int lx = lane & 7, ly = lane >> 3;
-      for (int st = wave; st < nst; st += TH / 64) {
-        int I64 = 0;
-        while ((I64 + 1) * (I64 + 2) <= st) ++I64;  // st -> (I64, J32), J32 <= 2·I64 + 1 (wave-uniform)
-        const int J32 = st - I64 * (I64 + 1);
-        const int ri = kb + 64 * I64 + ly, rj = kb + 32 * J32 + lx;
-        if (32 * J32 >= m) continue;  // past the trailing block (the last row tile's right half)
-        // the tile's old values are loaded ahead of the products (their latency hides behind the FMAs)
-        double acc[8][4], old[8][4];
+      if constexpr (NB % 4 == 0) {
+        // (r05) on the fp64 matrix cores: the wave's 64×32 tile is 4×2 blocks of v_mfma_f64_16x16x4f64
+        // (A = 16 panel rows × 4 columns, B = 4 columns × 16 panel rows, lane (l & 15, l >> 4) supplying
+        // element (row l & 15, column q + (l >> 4)) of each; D: column l & 15, rows (l >> 4) + 4·reg).  6 LDS reads
+        // per 8 MFMAs against the VALU form's 12 per 32 FMAs, which made that form LDS-bound; blocks wholly above
+        // the diagonal or past the trailing rows are skipped (wave-uniform).  Not bit-identical to the VALU form
+        // (the matrix core's product order), held to the oracle by the same tests.
+        const int lr = lane & 15, lk = lane >> 4;
+        for (int st = wave; st < nst; st += TH / 64) {
+          int I64 = 0;
+          while ((I64 + 1) * (I64 + 2) <= st) ++I64;
+          const int J32 = st - I64 * (I64 + 1);
+          const int ri0 = kb + 64 * I64, rj0 = kb + 32 * J32;
+          if (32 * J32 >= m) continue;
+          auto live = [&](int bi, int bj) {  // the block has a stored element (row >= column, both < rows)
+            return ri0 + 16 * bi < rows && rj0 + 16 * bj < rows && rj0 + 16 * bj <= ri0 + 16 * bi + 15;
+          };
+          double old[4][2][4];
 #pragma unroll
-        for (int a = 0; a < 8; ++a) {
-          const int rr = min(ri + 8 * a, rows - 1);
-          const double* row = M + at(k0 + rr, k0);
+          for (int bi = 0; bi < 4; ++bi)
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            acc[a][b] = 0.0;
-            old[a][b] = row[min(rj + 8 * b, rr)];  // clamped into the stored lower triangle
+            for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                const int rr = min(ri0 + 16 * bi + lk + 4 * g, rows - 1), cc = rj0 + 16 * bj + lr;
+                old[bi][bj][g] = M[at(k0 + rr, k0 + min(cc, rr))];  // clamped into the stored lower triangle
+              }
+          dx4 acc[4][2];
+#pragma unroll
+          for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = dx4{0.0, 0.0, 0.0, 0.0};
+          for (int q = 0; q < kb; q += 4) {
+            double a[4], b[2];
+#pragma unroll
+            for (int bi = 0; bi < 4; ++bi) a[bi] = PAN(min(ri0 + 16 * bi + lr, rows - 1), q + lk);
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) b[bj] = PAN(min(rj0 + 16 * bj + lr, rows - 1), q + lk);
+#pragma unroll
+            for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+              for (int bj = 0; bj < 2; ++bj)
+                if (live(bi, bj)) acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[bi], b[bj], acc[bi][bj], 0, 0, 0);
           }
+#pragma unroll
+          for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                const int r = ri0 + 16 * bi + lk + 4 * g, c = rj0 + 16 * bj + lr;
+                if (r < rows && c <= r) M[at(k0 + r, k0 + c)] = old[bi][bj][g] - acc[bi][bj][g];
+              }
         }
-        for (int q = 0; q < kb; ++q) {
-          double li[8], lj[4];
-#pragma unroll
-          for (int a = 0; a < 8; ++a) li[a] = PAN(min(ri + 8 * a, rows - 1), q);  // rows past n: clamped
-#pragma unroll
-          for (int b = 0; b < 4; ++b) lj[b] = PAN(min(rj + 8 * b, rows - 1), q);  // reads, masked below
-#pragma unroll
-          for (int a = 0; a < 8; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) acc[a][b] = fma(li[a], lj[b], acc[a][b]);
-        }
-#pragma unroll
-        for (int a = 0; a < 8; ++a) {
-          if (ri + 8 * a >= rows) continue;
-          double* row = M + at(k0 + ri + 8 * a, k0);
-#pragma unroll
-          for (int b = 0; b < 4; ++b)
-            if (rj + 8 * b < rows && rj + 8 * b <= ri + 8 * a) row[rj + 8 * b] = old[a][b] - acc[a][b];
+      } else {
+        for (int st = wave; st < nst; st += TH / 64) {
+          int I64 = 0;
+          while ((I64 + 1) * (I64 + 2) <= st) ++I64;  // st -> (I64, J32), J32 <= 2·I64 + 1 (wave-uniform)
+          const int J32 = st - I64 * (I64 + 1);
+          const int ri = kb + 64 * I64 + ly, rj = kb + 32 * J32 + lx;
+          if (32 * J32 >= m) continue;  // past the trailing block (the last row tile's right half)
+          // the tile's old values are loaded ahead of the products (their latency hides behind the FMAs)
+          double acc[8][4], old[8][4];
+  #pragma unroll
+          for (int a = 0; a < 8; ++a) {
+            const int rr = min(ri + 8 * a, rows - 1);
+            const double* row = M + at(k0 + rr, k0);
+  #pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              acc[a][b] = 0.0;
+              old[a][b] = row[min(rj + 8 * b, rr)];  // clamped into the stored lower triangle
+            }
+          }
+          for (int q = 0; q < kb; ++q) {
+            double li[8], lj[4];
+  #pragma unroll
+            for (int a = 0; a < 8; ++a) li[a] = PAN(min(ri + 8 * a, rows - 1), q);  // rows past n: clamped
+  #pragma unroll
+            for (int b = 0; b < 4; ++b) lj[b] = PAN(min(rj + 8 * b, rows - 1), q);  // reads, masked below
+  #pragma unroll
+            for (int a = 0; a < 8; ++a)
+  #pragma unroll
+              for (int b = 0; b < 4; ++b) acc[a][b] = fma(li[a], lj[b], acc[a][b]);
+          }
+  #pragma unroll
+          for (int a = 0; a < 8; ++a) {
+            if (ri + 8 * a >= rows) continue;
+            double* row = M + at(k0 + ri + 8 * a, k0);
+  #pragma unroll
+            for (int b = 0; b < 4; ++b)
+              if (rj + 8 * b < rows && rj + 8 * b <= ri + 8 * a) row[rj + 8 * b] = old[a][b] - acc[a][b];
+          }
         }
       }
       __syncthreads();
@@ -1305,6 +1363,18 @@ int gji_refine() {
 
 bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); }
 
+// Cholesky launch shape (measurement overrides, read once): RTI_RBF_CHOL_TH = 256 runs 256-thread workgroups
+// (NB <= 32 → 8 at most 32), RTI_RBF_CHOL_NB caps the panel width, RTI_RBF_CHOL_WPC = workgroups (and slots)
+// per CU
+struct ChCfg {
+  int th, nb, wpc;
+};
+ChCfg chol_cfg() {
+  static const ChCfg c = {env_int("RTI_RBF_CHOL_TH", RBF_CH_THREADS) == 256 ? 256 : RBF_CH_THREADS,
+                          std::max(1, env_int("RTI_RBF_CHOL_NB", 32)), std::max(1, env_int("RTI_RBF_CHOL_WPC", 1))};
+  return c;
+}
+
 // redo / fb_ws: the fallback's pixel list (redo[0] = count, zeroed) and its workspace, when uses_gji(N)
 template <typename T>
 void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
@@ -1314,10 +1384,11 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
   const dim3 g((unsigned)P);
   if (N > RBF_MAX_N) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
     const unsigned cg = (unsigned)(P < chol_grid ? P : chol_grid);
-    auto go = [&](auto kern) {
-      const size_t lds = chol_lds_bytes(N, chol_nb(N));
+    const ChCfg cf = chol_cfg();
+    auto go = [&](auto kern, int nb, int th) {
+      const size_t lds = chol_lds_bytes(N, nb);
       (void)reserve_lds(reinterpret_cast<const void*>(kern), lds);
-      hipLaunchKernelGGL(kern, dim3(cg), dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
+      hipLaunchKernelGGL(kern, dim3(cg), dim3(th), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
     };
     if (N > RBF_CH_MAX_N) {  // the panel below the diagonal block solved in place in the slot
       constexpr int NB = RBF_CH_GP_NB;
@@ -1326,13 +1397,22 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
       hipLaunchKernelGGL(kern, dim3(cg), dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
       return;
     }
-    switch (chol_nb(N)) {
-      case 32: go(rbf_solve_chol<32, T>); break;
-      case 16: go(rbf_solve_chol<16, T>); break;
-      case 8: go(rbf_solve_chol<8, T>); break;
-      case 4: go(rbf_solve_chol<4, T>); break;
-      case 2: go(rbf_solve_chol<2, T>); break;
-      default: go(rbf_solve_chol<1, T>); break;
+    const int nb = std::min(chol_nb(N), cf.nb);
+    if (cf.th == 256) {
+      switch (nb) {
+        case 32: go(rbf_solve_chol<32, T, false, 256>, 32, 256); break;
+        case 16: go(rbf_solve_chol<16, T, false, 256>, 16, 256); break;
+        default: go(rbf_solve_chol<8, T, false, 256>, 8, 256); break;
+      }
+      return;
+    }
+    switch (nb) {
+      case 32: go(rbf_solve_chol<32, T>, 32, RBF_CH_THREADS); break;
+      case 16: go(rbf_solve_chol<16, T>, 16, RBF_CH_THREADS); break;
+      case 8: go(rbf_solve_chol<8, T>, 8, RBF_CH_THREADS); break;
+      case 4: go(rbf_solve_chol<4, T>, 4, RBF_CH_THREADS); break;
+      case 2: go(rbf_solve_chol<2, T>, 2, RBF_CH_THREADS); break;
+      default: go(rbf_solve_chol<1, T>, 1, RBF_CH_THREADS); break;
     }
     return;
   }
@@ -1422,7 +1502,8 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   // + for the block solvers: the fp64 fallback's pixel list and (N > RBF_FB_LDS_N) per-workgroup matrices
   const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
-  int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
+  const int64_t ch_wg = (int64_t)device_cus() * chol_cfg().wpc;
+  int64_t chol_grid = chol ? (P < ch_wg ? P : ch_wg) : 0;
   const int64_t slot_doubles = N > RBF_CH_MAX_N ? chol_slot_doubles_gp(N) : chol_slot_doubles(N);
   if (chol && N > RBF_CH_MAX_N) {  // GP slots (≈ 4·N² bytes each): as many workgroups as RBF_GP_WS_BYTES holds
     const int64_t fit = (int64_t)(RBF_GP_WS_BYTES / ((size_t)slot_doubles * sizeof(double)));
