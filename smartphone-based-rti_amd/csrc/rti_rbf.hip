@@ -1104,11 +1104,23 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       const int kb = min(NB, n - k0), rows = n - k0;
       // stage the panel rows [k0, n), columns [k0, k0 + kb); a short last panel (kb < NB, then rows = kb) is
       // padded to NB rows and columns with the identity, so the diagonal block's code below runs unguarded
-      for (int idx = t; idx < (GP ? NB : max(rows, NB)) * NB; idx += TH) {  // (GP: the rest is in place)
-        const int r = idx / NB, c = idx - r * NB;
-        double v = r == c && r >= kb ? 1.0 : 0.0;
-        if (c < kb && c <= r && r < rows) v = M[at(k0 + r, k0 + c)];
-        pan[r * LDP + c] = v;
+      {  // (GP: the rest is in place); SU loads in flight per thread (r05: one at a time was latency-bound)
+        constexpr int SU = 8;
+        const int tot = (GP ? NB : max(rows, NB)) * NB;
+        for (int i0 = t; i0 < tot; i0 += SU * TH) {
+          double v[SU];
+#pragma unroll
+          for (int u = 0; u < SU; ++u) {
+            const int idx = i0 + u * TH, r = idx / NB, c = idx - r * NB;
+            v[u] = r == c && r >= kb ? 1.0 : 0.0;
+            if (idx < tot && c < kb && c <= r && r < rows) v[u] = M[at(k0 + r, k0 + c)];
+          }
+#pragma unroll
+          for (int u = 0; u < SU; ++u) {
+            const int idx = i0 + u * TH, r = idx / NB, c = idx - r * NB;
+            if (idx < tot) pan[r * LDP + c] = v[u];
+          }
+        }
       }
       __syncthreads();
       CH_MARK(4);
