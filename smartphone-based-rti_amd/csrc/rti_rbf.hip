@@ -1074,6 +1074,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         const double d = dist(i, j);
         rs += d;
         dup = dup || (j != i && d == 0.0);
+        if (!GP && j <= i && i < n) M[at(i, j)] = d;  // (r05) raw A, turned into S on its first read
       }
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
@@ -1092,9 +1093,21 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       const double ci = y1[i] - beta * u(i) * utb, mi = hah(n, i, i < n ? dist(n, i) : 0.0);
       cv[i] = ci, mv[i] = mi, y1[i] = ci, y2[i] = mi;
     }
-    // S = −(HAH)[:n, :n] into M, lower triangle, one wave per row (the distances again: a write-only pass)
-    for (int i = wave; i < n; i += TH / 64)
-      for (int j = lane; j <= i; j += 64) M[at(i, j)] = -hah(i, j, dist(i, j));
+    // S = −(HAH)[:n, :n]: (r05) M holds A's lower triangle from the row-sum pass, and the first panel's staging
+    // and trailing update (which between them read every element once) apply S = −hah(A) as they load it, with
+    // g copied into the LDS of the dead node coordinates — no second pass over the distances or over M.
+    // (GP, whose panel rows are read in place: the old write-only pass, the distances again.)
+    double* gl = reinterpret_cast<double*>(xs);  // [N] (xs, ys: 2N floats, dead from here on)
+    if constexpr (GP) {
+      for (int i = wave; i < n; i += TH / 64)
+        for (int j = lane; j <= i; j += 64) M[at(i, j)] = -hah(i, j, dist(i, j));
+    } else {
+      __syncthreads();  // every dist(n, i) above has read xs / ys
+      for (int i = t; i < N; i += TH) gl[i] = gv[i];
+    }
+    auto s_of = [&](int i, int j, double d) {  // hah's operations with g from LDS (bit-identical)
+      return -(d - beta * (u(i) * gl[j] + gl[i] * u(j)) + b2 * u(i) * u(j));
+    };
     __syncthreads();
     CH_MARK(3);
 
@@ -1114,6 +1127,13 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
             const int idx = i0 + u * TH, r = idx / NB, c = idx - r * NB;
             v[u] = r == c && r >= kb ? 1.0 : 0.0;
             if (idx < tot && c < kb && c <= r && r < rows) v[u] = M[at(k0 + r, k0 + c)];
+          }
+          if (!GP && k0 == 0) {  // first touch: A -> S
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+              const int idx = i0 + u * TH, r = idx / NB, c = idx - r * NB;
+              if (idx < tot && c < kb && c <= r && r < rows) v[u] = s_of(r, c, v[u]);
+            }
           }
 #pragma unroll
           for (int u = 0; u < SU; ++u) {
@@ -1222,6 +1242,16 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
                 const int rr = min(ri0 + 16 * bi + lk + 4 * g, rows - 1), cc = rj0 + 16 * bj + lr;
                 old[bi][bj][g] = M[at(k0 + rr, k0 + min(cc, rr))];  // clamped into the stored lower triangle
               }
+          if (!GP && k0 == 0)  // first touch: A -> S (the clamped elements are never stored)
+#pragma unroll
+            for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+              for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                  const int rr = min(ri0 + 16 * bi + lk + 4 * g, rows - 1), cc = rj0 + 16 * bj + lr;
+                  old[bi][bj][g] = s_of(rr, min(cc, rr), old[bi][bj][g]);
+                }
           dx4 acc[4][2];
 #pragma unroll
           for (int bi = 0; bi < 4; ++bi)
@@ -1266,6 +1296,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
             for (int b = 0; b < 4; ++b) {
               acc[a][b] = 0.0;
               old[a][b] = row[min(rj + 8 * b, rr)];  // clamped into the stored lower triangle
+              if (!GP && k0 == 0) old[a][b] = s_of(rr, min(rj + 8 * b, rr), old[a][b]);  // first touch: A -> S
             }
           }
           for (int q = 0; q < kb; ++q) {
@@ -1314,8 +1345,10 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         if (c == r) pan[r * LDP + NB] = 1.0 / l;
       }
       __syncthreads();
+      CH_MARK(11);
       if (wave == 0) diag_bwd(pan, kb, y1 + k0, y2 + k0);
       __syncthreads();
+      CH_MARK(12);
       // y[i] −= Σ_q L[k0+q][i]·z[k0+q]: rows of L, coalesced over i (z = 0 past a short block's end)
       auto upd = [&](int i, auto&& lval) {
         double s1 = y1[i], s2 = y2[i];
@@ -1330,6 +1363,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       if (t < k0) upd(t, [&](int q) { return lp[q]; });
       for (int i = t + TH; i < k0; i += TH) upd(i, [&](int q) { return M[at(k0 + min(q, kb - 1), i)]; });
       __syncthreads();
+      CH_MARK(13);
     }
     CH_MARK(9);
     // bordered elimination: y_n = (c_n + mᵀz1)/(μ + mᵀz2), y₁ = −z1 + z2·y_n, w = H y

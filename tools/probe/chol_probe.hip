@@ -57,10 +57,11 @@ int main(int argc, char** argv) {
   (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const int G = (int)(P < cus ? P : cus);
-  const char* names[11] = {"load", "A+rowsum", "g colsum", "c,m,S", "stage", "diag factor", "trsm+fwd diag",
-                           "writeback+fwd upd", "trailing", "backward", "final"};
+  const char* names[14] = {"load", "A+rowsum", "g colsum", "c,m,S", "stage", "diag factor", "trsm+fwd diag",
+                           "writeback+fwd upd", "trailing", "backward (rest)", "final", "  bwd: loads+stage",
+                           "  bwd: diag solve", "  bwd: update"};
   double tot = 0;
-  for (int k = 0; k < 11; ++k) {
+  for (int k = 0; k < 14; ++k) {
     double s = 0;
     for (int b = 0; b < G; ++b) s += (double)prof[b][k];
     const double us = s / G / ((double)P / G) / (rate_khz * 1e-3);  // µs per pixel (per workgroup)
