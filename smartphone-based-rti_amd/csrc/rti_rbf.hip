@@ -1257,7 +1257,8 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
           for (int bi = 0; bi < 4; ++bi)
 #pragma unroll
             for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = dx4{0.0, 0.0, 0.0, 0.0};
-          for (int q = 0; q < kb; q += 4) {
+#pragma unroll
+          for (int q = 0; q < NB; q += 4) {  // (kb = NB whenever there are trailing rows)
             double a[4], b[2];
 #pragma unroll
             for (int bi = 0; bi < 4; ++bi) a[bi] = PAN(min(ri0 + 16 * bi + lr, rows - 1), q + lk);
