@@ -204,7 +204,7 @@ int rti_fit_shared_q8(const void* op, int k, int N, const uint8_t* I, int64_t P,
  * of two per row: 22 significant bits) and fp32 accumulation (v_mfma_f32_16x16x32_f16): the accuracy of
  * the fp32 stream, a quarter of the q8 form's accumulator registers per pixel: 1024-pixel tiles with two
  * workgroups per CU for k <= 9 (when both fit in the LDS), else 2048-pixel tiles with one; kernel flags
- * (measurement): RTI_KERNEL_TILE_WAVES(1|2) forces the 2048- / 1024-pixel tile, RTI_KERNEL_CHUNKS(n) n tiles
+ * (measurement): RTI_KERNEL_TILE_WAVES(1|2|3) forces the 2048- / 1024-pixel tile / 2048 pixels on 16 waves, RTI_KERNEL_CHUNKS(n) n tiles
  * per workgroup, RTI_KERNEL_TILE_DEPTH(1|4|8) 16-pixel groups per read/MFMA round (all bit-identical).
  * rti_h16_operator builds the operator (rti_h16_operator_bytes(k, N)
  * bytes, device copy 16-byte aligned) from the fp64 pseudo-inverse (non-finite entries -> RTI_ERR_BAD_ARG).

@@ -45,12 +45,12 @@ __host__ __device__ constexpr int64_t h16_operator_bytes(int N) { return 2 * h16
 // Tile geometry: R pixels × STEP lights per step (v_mfma_f32_16x16x32_f16: 8 lights per lane), double-buffered
 // in LDS with a 16-byte row pad.  (A 4096-pixel × 16-light form on v_mfma_f32_16x16x16_f16 — 4-KiB runs, the
 // LDS the same — measured slower: c3 u8 0.228 vs 0.193 ms, it needs 128 accumulator VGPRs and spills.)
-template <int R, int STEP>
+template <int R, int STEP, int W = H16_W>
 struct H16Tile {
   static constexpr int RS = R + 16;           // LDS row stride: 16 consecutive rows span all 64 banks
-  static constexpr int WPX = R / H16_W;       // pixels per wave
+  static constexpr int WPX = R / W;           // pixels per wave
   static constexpr int G = WPX / 16;          // 16-pixel column groups per wave
-  static constexpr int PPW = STEP / H16_W;    // planes per wave and step
+  static constexpr int PPW = STEP / W;        // planes per wave and step
   static constexpr int LPP = R / 1024;        // 16-byte lane loads per plane
   static constexpr int NL = PPW * LPP;        // lane loads per step
   static constexpr size_t tile_bytes = (size_t)2 * STEP * RS;
@@ -101,16 +101,17 @@ __device__ __forceinline__ void h16_store(float* __restrict__ dst, int64_t P, in
 // PROBE (not reachable from the C ABI; tools/probe/h16_probe.hip): 1 = the coefficient stores dropped, 2 = the
 // stores non-temporal, 3 / 4 = (PTM-6, 1024-pixel tiles) each wave's 128 finished pixel rows staged in the free
 // half of the LDS tile and written back as three whole 1-KiB stores, plain / non-temporal
-template <int K, int LAYOUT, int R, int STEP, int CB = 1, int PROBE = 0>
-__global__ void __launch_bounds__(64 * H16_W)
+// W: waves per workgroup (8; 16 with the 2048-pixel tile = 2-KiB runs per plane and wave, measurement)
+template <int K, int LAYOUT, int R, int STEP, int CB = 1, int PROBE = 0, int W = H16_W>
+__global__ void __launch_bounds__(64 * W)
 fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __restrict__ I, int64_t pb, int64_t pe,
         int tpw, int64_t P, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
-  using TL = H16Tile<R, STEP>;
+  using TL = H16Tile<R, STEP, W>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int T = (N + STEP - 1) / STEP, Np = h16_npad(N);
   unsigned char* __restrict__ lop = lds;                           // hi[16][Np], lo[16][Np] fp16, inv_s[16]
   unsigned char* __restrict__ tile = lds + h16_operator_bytes(N);   // [2][STEP][RS]
-  for (int i = threadIdx.x; i < (int)(h16_operator_bytes(N) / 16); i += 64 * H16_W)
+  for (int i = threadIdx.x; i < (int)(h16_operator_bytes(N) / 16); i += 64 * W)
     *reinterpret_cast<v4i*>(lop + 16 * i) = *reinterpret_cast<const v4i*>(op + 16 * i);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -123,18 +124,24 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
   auto tile_px = [&](int ti) { return pb + ((int64_t)ti * G + blockIdx.x) * R; };
   const unsigned char* __restrict__ src = I + (int64_t)blockIdx.y * cstride;
 
+  // Planes past N (the last step's padding to 32 lights) carry zero weights: their loads are buffer loads with
+  // num_records 0 — zeros, no memory access (r04 re-read plane N − 1: 28 % of c3's load instructions went to the
+  // cache for nothing) — and the instruction stream keeps its fixed shape for the counted waits.
+  const uint32_t recs = (uint32_t)min(pe, (int64_t)0x7fffffff);
   auto load = [&](int s, v4i (&st)[TL::NL]) {
     const int ti = s / T, t = s - ti * T;
     const int64_t px0 = tile_px(ti) + 16 * lane;
 #pragma unroll
     for (int j = 0; j < TL::PPW; ++j) {
-      int n = t * STEP + TL::PPW * wave + j;
-      n = n < N ? n : N - 1;  // lights past N carry zero weights
+      const int n = t * STEP + TL::PPW * wave + j;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<unsigned char*>(src + (int64_t)(n < N ? n : 0) * lstride), (short)0, n < N ? (int)recs : 0,
+          0x00020000);
 #pragma unroll
       for (int h = 0; h < TL::LPP; ++h) {
         int64_t px = px0 + 1024 * h;
         px = px < pe ? px : pe - 16;  // lanes past the image re-read its last 16 pixels (never stored)
-        st[j * TL::LPP + h] = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(src + (int64_t)n * lstride + px));
+        st[j * TL::LPP + h] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)px, 0, 2);  // (2: non-temporal)
       }
     }
   };
@@ -298,7 +305,7 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
     finish(ntiles - 1);
 }
 
-template <int K, int LAYOUT, int R, int STEP>
+template <int K, int LAYOUT, int R, int STEP, int W = H16_W>
 int launch_h16_t(const unsigned char* op, int N, const unsigned char* I, int64_t P, int C, int64_t ls, int64_t cs,
                  float* coef, int64_t ocs, int tpw, int cb, hipStream_t s) {
   const size_t lds = h16_lds_bytes<R, STEP>(N);
@@ -306,12 +313,14 @@ int launch_h16_t(const unsigned char* op, int N, const unsigned char* I, int64_t
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_h16: LDS of %zu B (N=%d) exceeds 160 KiB", lds, N);
   // AUTO batches 4 groups per read/MFMA round (c2 u8 0.0379 against 0.0443 ms one group at a time, c3 / c4 u8
   // within 1 %: profiles/r04z_h16_batch_sweep_c*.log); RTI_KERNEL_TILE_DEPTH(1|8) for measurement
-  auto kern = cb == 8 ? fit_h16<K, LAYOUT, R, STEP, 8> : cb == 1 ? fit_h16<K, LAYOUT, R, STEP, 1> : fit_h16<K, LAYOUT, R, STEP, 4>;
+  auto kern = cb == 8   ? fit_h16<K, LAYOUT, R, STEP, 8, 0, W>
+              : cb == 1 ? fit_h16<K, LAYOUT, R, STEP, 1, 0, W>
+                        : fit_h16<K, LAYOUT, R, STEP, 4, 0, W>;
   if (reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_h16: cannot reserve %zu B of LDS", lds);
   const int64_t tiles = (P + R - 1) / R;
   const dim3 grid((unsigned)((tiles + tpw - 1) / tpw), C);
-  hipLaunchKernelGGL(kern, grid, dim3(64 * H16_W), lds, s, op, N, I, (int64_t)0, P, tpw, P, ls, cs, coef, ocs);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * W), lds, s, op, N, I, (int64_t)0, P, tpw, P, ls, cs, coef, ocs);
   return check_launch("rti_fit_shared_h16");
 }
 
@@ -327,16 +336,16 @@ struct H16Args {
   int want;  // RTI_KERNEL_CHUNKS: tiles per workgroup (0 = AUTO)
   int cb;    // RTI_KERNEL_TILE_DEPTH: batched groups (measurement)
   hipStream_t s;
-  int geom = 0;  // RTI_KERNEL_TILE_WAVES: 0 AUTO, 1 the 2048-pixel tile, 2 the 1024-pixel tile (measurement)
+  int geom = 0;  // RTI_KERNEL_TILE_WAVES: 0 AUTO, 1 the 2048-pixel tile on 8 waves, 2 the 1024-pixel tile, 3 2048 on 16
 };
 
-template <int K, int LAYOUT, int R, int STEP>
+template <int K, int LAYOUT, int R, int STEP, int W = H16_W>
 int launch_h16_g(const H16Args& a) {
   // one workgroup per CU over all channels, each streaming tpw interleaved tiles
   const int64_t tpc = (a.P + R - 1) / R, cus = device_cus();
   const int64_t wpc = (cus >= a.C ? cus / a.C : 1) * (2048 / R);  // workgroups per channel: 2048/R per CU
   const int tpw = a.want ? a.want : (int)((tpc + wpc - 1) / wpc);
-  return launch_h16_t<K, LAYOUT, R, STEP>(a.op, a.N, a.I, a.P, a.C, a.ls, a.cs, a.coef, a.ocs, tpw, a.cb, a.s);
+  return launch_h16_t<K, LAYOUT, R, STEP, W>(a.op, a.N, a.I, a.P, a.C, a.ls, a.cs, a.coef, a.ocs, tpw, a.cb, a.s);
 }
 
 // AUTO geometry: 1024-pixel tiles (1-KiB runs per wave and plane, two workgroups per CU) for k <= 9 where two
@@ -350,6 +359,11 @@ bool h16_half_tiles(int k, int N, int geom) {
 
 template <int K>
 int launch_h16_l(int layout, const H16Args& a) {
+  // the 2048-pixel tile on 16 waves (2-KiB runs per plane and wave; AUTO where the 1024-pixel tile is not):
+  // c4 u8 1.282 vs 1.308 ms on 8 waves, c3 u8 0.1866 vs 0.1866 on 1024-pixel tiles (profiles/r05w_h16_geometry_*)
+  if (a.geom == 3 || (a.geom == 0 && !h16_half_tiles(K, a.N, 0)))
+    return layout == RTI_COEF_PLANAR ? launch_h16_g<K, RTI_COEF_PLANAR, 2048, 32, 16>(a)
+                                     : launch_h16_g<K, RTI_COEF_PIXEL_MAJOR, 2048, 32, 16>(a);
   if (h16_half_tiles(K, a.N, a.geom))
     return layout == RTI_COEF_PLANAR ? launch_h16_g<K, RTI_COEF_PLANAR, 1024, 32>(a)
                                      : launch_h16_g<K, RTI_COEF_PIXEL_MAJOR, 1024, 32>(a);
@@ -424,11 +438,13 @@ extern "C" int rti_fit_shared_h16(const void* op, int k, int N, const uint8_t* I
   if (ls < P) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_h16: light_stride < P");
   if (C > 1 && cs < (int64_t)N * ls) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_h16: channel_stride");
   if (C > 1 && ocs < P * k) return fail(RTI_ERR_BAD_ARG, "rti_fit_shared_h16: coef_channel_stride");
+  if (P > 0x7fffff00)  // plane offsets are 32-bit buffer offsets
+    return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_h16: P=%lld pixels per plane", (long long)P);
   if (P % 16 || ls % 16 || cs % 16 || !aligned_to(I, 16) || !aligned_to(op, 16) || !aligned_to(coef, 16) || ocs % 4)
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_h16: needs P, strides and pointers 16-byte aligned");
   note_launches(1);
   // RTI_KERNEL_CHUNKS(n): tiles per workgroup = n; RTI_KERNEL_TILE_DEPTH(1|4|8): groups batched per round;
-  // RTI_KERNEL_TILE_WAVES(1|2): the 2048- or 1024-pixel tile (measurement)
+  // RTI_KERNEL_TILE_WAVES(1|2|3): the 2048- or 1024-pixel tile, or 2048 pixels on 16 waves (measurement)
   const H16Args a{static_cast<const unsigned char*>(op), N, I, P, C, ls, cs, coef, ocs,
                   (kernel >> RTI_KERNEL_CHUNKS_SHIFT) & 0xF, (kernel >> RTI_KERNEL_TILE_DEPTH_SHIFT) & 0xF,
                   (hipStream_t)stream, (kernel >> RTI_KERNEL_TILE_WAVES_SHIFT) & 0xF};

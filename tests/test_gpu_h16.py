@@ -97,10 +97,11 @@ def test_tile_streams_bit_identical(cuda):
         g = torch.Generator(device=cuda).manual_seed(5)
         I = torch.randint(0, 256, (C, N, P), generator=g, device=cuda, dtype=torch.uint8)
         outs = []
-        W = L.RTI_KERNEL_TILE_WAVES_SHIFT  # tile geometry: 1 = 2048 pixels, 2 = 1024 pixels (AUTO for k <= 9)
+        W = L.RTI_KERNEL_TILE_WAVES_SHIFT  # geometry: 1 = 2048 px / 8 waves, 2 = 1024 px (AUTO k <= 9), 3 = 2048 / 16
         for flags in (0, 1 << L.RTI_KERNEL_CHUNKS_SHIFT, 3 << L.RTI_KERNEL_CHUNKS_SHIFT,
                       4 << L.RTI_KERNEL_TILE_DEPTH_SHIFT, 8 << L.RTI_KERNEL_TILE_DEPTH_SHIFT,  # batched groups
-                      1 << W, 2 << W, (2 << W) | (1 << L.RTI_KERNEL_CHUNKS_SHIFT), (1 << W) | (3 << L.RTI_KERNEL_CHUNKS_SHIFT)):
+                      1 << W, 2 << W, (2 << W) | (1 << L.RTI_KERNEL_CHUNKS_SHIFT), (1 << W) | (3 << L.RTI_KERNEL_CHUNKS_SHIFT),
+                      3 << W, (3 << W) | (3 << L.RTI_KERNEL_CHUNKS_SHIFT)):  # 3: 2048 pixels on 16 waves (r05)
             coef = torch.full((C, P, k), float("nan"), device=cuda)
             rti.api.fit_h16_into(op, I, coef, k=k, flags=flags)
             outs.append(coef)
@@ -163,7 +164,7 @@ def test_geometries_at_max_lights(cuda, basis):
     I = torch.randint(0, 256, (Nmax, P), generator=torch.Generator(device=cuda).manual_seed(7), device=cuda,
                       dtype=torch.uint8)
     outs = []
-    for geom in (0, 1, 2):
+    for geom in (0, 1, 2, 3):
         coef = torch.full((1, P, k), float("nan"), device=cuda)
         rti.api.fit_h16_into(op, I, coef, k=k, flags=geom << L.RTI_KERNEL_TILE_WAVES_SHIFT)
         outs.append(coef)

@@ -13,7 +13,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "smartphone-based-rti_amd"))
+sys.path.insert(0, os.environ.get("RTI_PKG_DIR", os.path.join(ROOT, "smartphone-based-rti_amd")))  # A/B builds
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
@@ -41,12 +41,13 @@ def main():
     coef = torch.empty((C, P, k), device=dev)
     ref = torch.empty((C, P, k), device=dev)
     variants = []
-    for half in (1, 2):  # RTI_KERNEL_TILE_WAVES: 1 = 2048-pixel tiles (one workgroup per CU), 2 = 1024 (two)
+    geoms = {1: "2048px", 2: "1024px", 3: "2048px16w"}
+    for half in (1, 2, 3):  # RTI_KERNEL_TILE_WAVES: 1 = 2048-pixel tiles (one workgroup per CU), 2 = 1024 (two), 3 = 2048 on 16 waves
         for tpw in [int(x) for x in args.tpw.split(",")]:
             for cb in [int(x) for x in args.batches.split(",") if x]:  # groups batched per step (TILE_DEPTH)
                 fl = (tpw << L.RTI_KERNEL_CHUNKS_SHIFT) | (cb << L.RTI_KERNEL_TILE_DEPTH_SHIFT) | \
                      (half << L.RTI_KERNEL_TILE_WAVES_SHIFT)
-                variants.append((f"h16_{'1024px' if half == 2 else '2048px'}_tpw{tpw or 'auto'}_batch{cb}",
+                variants.append((f"h16_{geoms[half]}_tpw{tpw or 'auto'}_batch{cb}",
                                  lambda fl=fl: rti.api.fit_h16_into(op, I8, coef, k=k, layout="pixel", flags=fl)))
     probe = os.path.join(ROOT, "tools", "probe", "libh16_probe.so")
     if C == 1 and os.path.exists(probe):  # tools/probe/h16_probe.hip: the library kernel with its stores dropped
