@@ -124,24 +124,19 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
   auto tile_px = [&](int ti) { return pb + ((int64_t)ti * G + blockIdx.x) * R; };
   const unsigned char* __restrict__ src = I + (int64_t)blockIdx.y * cstride;
 
-  // Planes past N (the last step's padding to 32 lights) carry zero weights: their loads are buffer loads with
-  // num_records 0 — zeros, no memory access (r04 re-read plane N − 1: 28 % of c3's load instructions went to the
-  // cache for nothing) — and the instruction stream keeps its fixed shape for the counted waits.
-  const uint32_t recs = (uint32_t)min(pe, (int64_t)0x7fffffff);
   auto load = [&](int s, v4i (&st)[TL::NL]) {
     const int ti = s / T, t = s - ti * T;
     const int64_t px0 = tile_px(ti) + 16 * lane;
 #pragma unroll
     for (int j = 0; j < TL::PPW; ++j) {
-      const int n = t * STEP + TL::PPW * wave + j;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<unsigned char*>(src + (int64_t)(n < N ? n : 0) * lstride), (short)0, n < N ? (int)recs : 0,
-          0x00020000);
+      int n = t * STEP + TL::PPW * wave + j;
+      n = n < N ? n : N - 1;  // lights past N carry zero weights (re-reads of plane N − 1: L2 hits; zero-record
+                              // buffer loads in their place measured flat, profiles/r05v_h16_ab_*, r05f_*)
 #pragma unroll
       for (int h = 0; h < TL::LPP; ++h) {
         int64_t px = px0 + 1024 * h;
         px = px < pe ? px : pe - 16;  // lanes past the image re-read its last 16 pixels (never stored)
-        st[j * TL::LPP + h] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)px, 0, 2);  // (2: non-temporal)
+        st[j * TL::LPP + h] = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(src + (int64_t)n * lstride + px));
       }
     }
   };
