@@ -1068,17 +1068,36 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
     // A's row sums (one wave per row; every distance of the row, so no column pass over a stored A) and the
     // repeated-node check (SciPy: LinAlgError); g = A u = e·(row sums) − A[:, n]
     bool dup = false;
-    for (int i = wave; i < N; i += TH / 64) {
-      double rs = 0.0;
+    // (r05) RB rows per wave at a time: RB independent sqrt chains and butterflies in flight, each column's node
+    // read once per RB rows (the same rows per wave and the same order of additions per row: bit-identical)
+    constexpr int RB = 4, WV = TH / 64;
+    for (int i0 = wave; i0 < N; i0 += RB * WV) {
+      double rs[RB], xi[RB], yi[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int i = min(i0 + r * WV, N - 1);
+        xi[r] = (double)xs[i], yi[r] = (double)ys[i], rs[r] = 0.0;
+      }
       for (int j = lane; j < N; j += 64) {
-        const double d = dist(i, j);
-        rs += d;
-        dup = dup || (j != i && d == 0.0);
-        if (!GP && j <= i && i < n) M[at(i, j)] = d;  // (r05) raw A, turned into S on its first read
+        const double xj = (double)xs[j], yj = (double)ys[j];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int i = i0 + r * WV;
+          const double d = dist64(xi[r], yi[r], xj, yj);
+          rs[r] += d;
+          dup = dup || (i < N && j != i && d == 0.0);
+          if (!GP && j <= i && i < n) M[at(i, j)] = d;  // raw A, turned into S on its first read
+        }
       }
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
-      if (lane == 0) gv[i] = fma(e, rs, -(i < n ? dist(n, i) : 0.0));
+      for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int r = 0; r < RB; ++r) rs[r] += __shfl_xor(rs[r], off, 64);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int i = i0 + r * WV;
+        if (lane == 0 && i < N) gv[i] = fma(e, rs[r], -(i < n ? dist(n, i) : 0.0));
+      }
     }
     if (dup) s_bad = 1;
     __syncthreads();
