@@ -98,7 +98,8 @@ __device__ __forceinline__ void h16_store(float* __restrict__ dst, int64_t P, in
 }
 
 // CB: 16-pixel groups whose reads and MFMAs are batched per step (AUTO 4; 1 one group at a time)
-// PROBE (not reachable from the C ABI; tools/probe/h16_probe.hip): 1 = the coefficient stores dropped, 2 = the
+// PROBE (not reachable from the C ABI; tools/probe/h16_probe.hip): 5 / 6 = as 1 with the transposed reads and
+// MFMAs dropped / with those and the LDS parking dropped (the load pipeline alone); 1 = the coefficient stores dropped, 2 = the
 // stores non-temporal, 3 / 4 = (PTM-6, 1024-pixel tiles) each wave's 128 finished pixel rows staged in the free
 // half of the LDS tile and written back as three whole 1-KiB stores, plain / non-temporal
 // W: waves per workgroup (8; 16 with the 2048-pixel tile = 2-KiB runs per plane and wave, measurement)
@@ -140,7 +141,13 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
       }
     }
   };
+  int sink = 0;  // PROBE 6: the loads' use when nothing is parked
   auto park = [&](int b, const v4i (&st)[TL::NL]) {
+    if constexpr (PROBE == 6) {
+#pragma unroll
+      for (int j = 0; j < TL::NL; ++j) sink ^= st[j][0] ^ st[j][3];
+      return;
+    }
     unsigned char* tb = tile + b * (STEP * TL::RS) + (TL::PPW * wave) * TL::RS + 16 * lane;
 #pragma unroll
     for (int j = 0; j < TL::PPW; ++j)
@@ -163,6 +170,7 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
   const int roff = (8 * g + ((lane & 15) >> 1)) * TL::RS + 8 * (lane & 1) + TL::WPX * wave;
   const int arow = (lane & 15) * Np + 8 * g;
   auto compute = [&](int b, int t) {
+    if constexpr (PROBE == 5 || PROBE == 6) return;  // (probe: no transposed reads, no MFMAs)
     const unsigned char* tb = tile + b * (STEP * TL::RS) + roff;
     const half8 ah = *reinterpret_cast<const half8*>(lop + 2 * (arow + t * STEP));
     const half8 al = *reinterpret_cast<const half8*>(lop + h16_half_bytes(N) + 2 * (arow + t * STEP));
@@ -210,8 +218,8 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[c][r] * sc[r];
-        if constexpr (PROBE == 1) {
-          if (v[0] + v[1] + v[2] + v[3] == -1.2345f) dst[0] = v[0];  // keeps the arithmetic alive
+        if constexpr (PROBE == 1 || PROBE == 5 || PROBE == 6) {
+          if (v[0] + v[1] + v[2] + v[3] == -1.2345f || sink == 0x7a5a5a5b) dst[0] = v[0];  // keeps the work alive
         } else {
           h16_store<K, LAYOUT, PROBE == 2>(dst, P, p, g, v);
         }

@@ -55,6 +55,8 @@ extern "C" int h16_probe(const void* op, int k, int N, const void* I, int64_t P,
       case 2: return probe_t<6, 2>(o, N, x, P, coef, s);
       case 3: return probe_t<6, 3>(o, N, x, P, coef, s);
       case 4: return probe_t<6, 4>(o, N, x, P, coef, s);
+      case 5: return probe_t<6, 5>(o, N, x, P, coef, s);
+      case 6: return probe_t<6, 6>(o, N, x, P, coef, s);
       default: return probe_t<6, 0>(o, N, x, P, coef, s);
     }
   if (k == 16)

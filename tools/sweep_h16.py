@@ -65,13 +65,16 @@ def main():
         if k == 6:
             variants.append(("probe_h16_staged", lambda: pr(3)))
             variants.append(("probe_h16_staged_nt", lambda: pr(4)))
+            variants.append(("probe_h16_loads_park", lambda: pr(5)))  # no stores, no transposed reads / MFMAs
+            variants.append(("probe_h16_loads_only", lambda: pr(6)))  # ... and no LDS parking
     rti.api.fit_h16_into(op, I8, ref, k=k, layout="pixel")
     same = {}
     for name, fn in variants:
         coef.fill_(float("nan"))
         fn()
         torch.cuda.synchronize()
-        same[name] = bool(torch.equal(coef, ref)) if name != "probe_h16_nostores" else None
+        same[name] = bool(torch.equal(coef, ref)) if name not in ("probe_h16_nostores", "probe_h16_loads_park",
+                                                                   "probe_h16_loads_only") else None
     stream = torch.cuda.current_stream(dev)
     times = {name: [] for name, _ in variants}
     for _ in range(args.rounds):
