@@ -980,9 +980,10 @@ __device__ unsigned long long rti_chol_prof[1024][16];
 // GP (N > RBF_CH_MAX_N, whose one-column panel no longer fits the LDS): the same algorithm with only the NB×NB
 // diagonal block in LDS; the panel rows below it are read and solved in place in the slot's packed L (they ARE
 // the panel), and the right-hand sides and nodes live in the slot too (chol_slot_doubles_gp).
-// TH: threads per workgroup (AUTO 512, one workgroup per CU; 256 = two per CU, measurement: RTI_RBF_CHOL_TH)
+// TH: threads per workgroup, one workgroup per CU (r05 measured 256-thread workgroups two per CU, NB = 16:
+// 527 vs 441 ms at N = 400, profiles/r05m_chol_shape_sweep.log)
 template <int NB, typename T, bool GP = false, int TH = RBF_CH_THREADS>
-__global__ void __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(TH == 256 ? 2 : 1)))
+__global__ void __launch_bounds__(TH)
 rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
                double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status,
                double* __restrict__ ws) {
@@ -1429,18 +1430,6 @@ int gji_refine() {
 
 bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); }
 
-// Cholesky launch shape (measurement overrides, read once): RTI_RBF_CHOL_TH = 256 runs 256-thread workgroups
-// (NB <= 32 → 8 at most 32), RTI_RBF_CHOL_NB caps the panel width, RTI_RBF_CHOL_WPC = workgroups (and slots)
-// per CU
-struct ChCfg {
-  int th, nb, wpc;
-};
-ChCfg chol_cfg() {
-  static const ChCfg c = {env_int("RTI_RBF_CHOL_TH", RBF_CH_THREADS) == 256 ? 256 : RBF_CH_THREADS,
-                          std::max(1, env_int("RTI_RBF_CHOL_NB", 32)), std::max(1, env_int("RTI_RBF_CHOL_WPC", 1))};
-  return c;
-}
-
 // redo / fb_ws: the fallback's pixel list (redo[0] = count, zeroed) and its workspace, when uses_gji(N)
 template <typename T>
 void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_t P, double* wT, float2* xyT,
@@ -1450,11 +1439,10 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
   const dim3 g((unsigned)P);
   if (N > RBF_MAX_N) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
     const unsigned cg = (unsigned)(P < chol_grid ? P : chol_grid);
-    const ChCfg cf = chol_cfg();
-    auto go = [&](auto kern, int nb, int th) {
+    auto go = [&](auto kern, int nb) {
       const size_t lds = chol_lds_bytes(N, nb);
       (void)reserve_lds(reinterpret_cast<const void*>(kern), lds);
-      hipLaunchKernelGGL(kern, dim3(cg), dim3(th), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
+      hipLaunchKernelGGL(kern, dim3(cg), dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
     };
     if (N > RBF_CH_MAX_N) {  // the panel below the diagonal block solved in place in the slot
       constexpr int NB = RBF_CH_GP_NB;
@@ -1463,22 +1451,14 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
       hipLaunchKernelGGL(kern, dim3(cg), dim3(RBF_CH_THREADS), lds, s, lu, lv, In, N, P, wT, xyT, status, fb_ws);
       return;
     }
-    const int nb = std::min(chol_nb(N), cf.nb);
-    if (cf.th == 256) {
-      switch (nb) {
-        case 32: go(rbf_solve_chol<32, T, false, 256>, 32, 256); break;
-        case 16: go(rbf_solve_chol<16, T, false, 256>, 16, 256); break;
-        default: go(rbf_solve_chol<8, T, false, 256>, 8, 256); break;
-      }
-      return;
-    }
+    const int nb = chol_nb(N);
     switch (nb) {
-      case 32: go(rbf_solve_chol<32, T>, 32, RBF_CH_THREADS); break;
-      case 16: go(rbf_solve_chol<16, T>, 16, RBF_CH_THREADS); break;
-      case 8: go(rbf_solve_chol<8, T>, 8, RBF_CH_THREADS); break;
-      case 4: go(rbf_solve_chol<4, T>, 4, RBF_CH_THREADS); break;
-      case 2: go(rbf_solve_chol<2, T>, 2, RBF_CH_THREADS); break;
-      default: go(rbf_solve_chol<1, T>, 1, RBF_CH_THREADS); break;
+      case 32: go(rbf_solve_chol<32, T>, 32); break;
+      case 16: go(rbf_solve_chol<16, T>, 16); break;
+      case 8: go(rbf_solve_chol<8, T>, 8); break;
+      case 4: go(rbf_solve_chol<4, T>, 4); break;
+      case 2: go(rbf_solve_chol<2, T>, 2); break;
+      default: go(rbf_solve_chol<1, T>, 1); break;
     }
     return;
   }
@@ -1568,8 +1548,7 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   // + for the block solvers: the fp64 fallback's pixel list and (N > RBF_FB_LDS_N) per-workgroup matrices
   const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
-  const int64_t ch_wg = (int64_t)device_cus() * chol_cfg().wpc;
-  int64_t chol_grid = chol ? (P < ch_wg ? P : ch_wg) : 0;
+  int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
   const int64_t slot_doubles = N > RBF_CH_MAX_N ? chol_slot_doubles_gp(N) : chol_slot_doubles(N);
   if (chol && N > RBF_CH_MAX_N) {  // GP slots (≈ 4·N² bytes each): as many workgroups as RBF_GP_WS_BYTES holds
     const int64_t fit = (int64_t)(RBF_GP_WS_BYTES / ((size_t)slot_doubles * sizeof(double)));
