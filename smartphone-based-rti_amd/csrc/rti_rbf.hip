@@ -1069,35 +1069,97 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
     // A's row sums (one wave per row; every distance of the row, so no column pass over a stored A) and the
     // repeated-node check (SciPy: LinAlgError); g = A u = e·(row sums) − A[:, n]
     bool dup = false;
-    // (r05) RB rows per wave at a time: RB independent sqrt chains and butterflies in flight, each column's node
-    // read once per RB rows (the same rows per wave and the same order of additions per row: bit-identical)
-    constexpr int RB = 4, WV = TH / 64;
-    for (int i0 = wave; i0 < N; i0 += RB * WV) {
-      double rs[RB], xi[RB], yi[RB];
+    // (r05) SYMMETRIC form where its partial sums fit in the (still unused) panel LDS: each distance of the
+    // lower triangle once, in 64×64 tiles (lane = column, rows in chunks of 8): the column partials stay in
+    // registers, the row partials are transposed through a per-wave LDS slice; per tile they go to LDS and
+    // every row's sum is added up in a fixed order (deterministic).  Diagonal tiles are computed whole (their
+    // row partials cover both halves); A's lower triangle is stored coalesced on the way.
+    const int T64r = (N + 63) / 64, ntl = T64r * (T64r + 1) / 2;
+    const bool sym = !GP && (size_t)ntl * 1024 + (size_t)(TH / 64) * 8 * 64 * 8 <= (size_t)N * LDP * 8;
+    if (sym) {
+      double* rowp = pan;                         // [ntl][64]
+      double* colp = rowp + (size_t)ntl * 64;     // [ntl][64]
+      double* rbuf = colp + (size_t)ntl * 64 + wave * (8 * 64);  // [8][64] per wave
+      for (int st = wave; st < ntl; st += TH / 64) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= st) ++I;
+        const int J = st - I * (I + 1) / 2;
+        const int j = 64 * J + lane;
+        const bool jv = j < N;
+        const double xj = (double)xs[jv ? j : 0], yj = (double)ys[jv ? j : 0];
+        double cacc = 0.0;
+        const int rows_t = min(64, N - 64 * I);
+        for (int m0 = 0; m0 < rows_t; m0 += 8) {
+          double v[8];
 #pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const int i = min(i0 + r * WV, N - 1);
-        xi[r] = (double)xs[i], yi[r] = (double)ys[i], rs[r] = 0.0;
+          for (int q = 0; q < 8; ++q) {
+            const int i = 64 * I + m0 + q;
+            const bool iv = i < N;
+            const double d = dist64((double)xs[iv ? i : 0], (double)ys[iv ? i : 0], xj, yj);
+            const double dd = iv && jv ? d : 0.0;
+            v[q] = dd;
+            if (I > J) cacc += dd;
+            dup = dup || (iv && jv && j != i && d == 0.0);
+            if (iv && jv && j <= i && i < n) M[at(i, j)] = d;  // raw A, turned into S on its first read
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) rbuf[q * 64 + lane] = v[q];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const int q = lane & 7, sg = lane >> 3;  // row q of the chunk, columns 8·sg .. 8·sg + 7
+          double rsum = 0.0;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) rsum += rbuf[q * 64 + 8 * sg + c];
+          rsum += __shfl_xor(rsum, 8, 64);
+          rsum += __shfl_xor(rsum, 16, 64);
+          rsum += __shfl_xor(rsum, 32, 64);
+          if (lane < 8) rowp[(size_t)st * 64 + m0 + q] = rsum;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the reads before the next chunk's writes
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (I > J) colp[(size_t)st * 64 + lane] = cacc;
       }
-      for (int j = lane; j < N; j += 64) {
-        const double xj = (double)xs[j], yj = (double)ys[j];
-#pragma unroll
+      __syncthreads();
+      for (int i = t; i < N; i += TH) {  // row i: its row-block's row partials, then the column partials below
+        const int I = i >> 6, r = i & 63;
+        double rs = 0.0;
+        for (int J = 0; J <= I; ++J) rs += rowp[(size_t)(I * (I + 1) / 2 + J) * 64 + r];
+        for (int I2 = I + 1; I2 < T64r; ++I2) rs += colp[(size_t)(I2 * (I2 + 1) / 2 + I) * 64 + r];
+        gv[i] = fma(e, rs, -(i < n ? dist(n, i) : 0.0));
+      }
+    } else {
+      // (r05) RB rows per wave at a time: RB independent sqrt chains and butterflies in flight, each column's node
+      // read once per RB rows (the same rows per wave and the same order of additions per row: bit-identical)
+      constexpr int RB = 4, WV = TH / 64;
+      for (int i0 = wave; i0 < N; i0 += RB * WV) {
+        double rs[RB], xi[RB], yi[RB];
+  #pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int i = min(i0 + r * WV, N - 1);
+          xi[r] = (double)xs[i], yi[r] = (double)ys[i], rs[r] = 0.0;
+        }
+        for (int j = lane; j < N; j += 64) {
+          const double xj = (double)xs[j], yj = (double)ys[j];
+  #pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const int i = i0 + r * WV;
+            const double d = dist64(xi[r], yi[r], xj, yj);
+            rs[r] += d;
+            dup = dup || (i < N && j != i && d == 0.0);
+            if (!GP && j <= i && i < n) M[at(i, j)] = d;  // raw A, turned into S on its first read
+          }
+        }
+  #pragma unroll
+        for (int off = 32; off >= 1; off >>= 1)
+  #pragma unroll
+          for (int r = 0; r < RB; ++r) rs[r] += __shfl_xor(rs[r], off, 64);
+  #pragma unroll
         for (int r = 0; r < RB; ++r) {
           const int i = i0 + r * WV;
-          const double d = dist64(xi[r], yi[r], xj, yj);
-          rs[r] += d;
-          dup = dup || (i < N && j != i && d == 0.0);
-          if (!GP && j <= i && i < n) M[at(i, j)] = d;  // raw A, turned into S on its first read
+          if (lane == 0 && i < N) gv[i] = fma(e, rs[r], -(i < n ? dist(n, i) : 0.0));
         }
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1)
-#pragma unroll
-        for (int r = 0; r < RB; ++r) rs[r] += __shfl_xor(rs[r], off, 64);
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const int i = i0 + r * WV;
-        if (lane == 0 && i < N) gv[i] = fma(e, rs[r], -(i < n ? dist(n, i) : 0.0));
       }
     }
     if (dup) s_bad = 1;
