@@ -1304,62 +1304,66 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         // per 8 MFMAs against the VALU form's 12 per 32 FMAs, which made that form LDS-bound; blocks wholly above
         // the diagonal or past the trailing rows are skipped (wave-uniform).  Not bit-identical to the VALU form
         // (the matrix core's product order), held to the oracle by the same tests.
+        // (r05) 32×32 wave tiles (2×2 blocks): twice the 64×32 form's tiles to balance over the waves, and
+        // half its accumulators (no spills at NB <= 16): 346.3 vs 352.8 ms at N = 400, bit-identical
+        // (profiles/r05ak_chol_ab_32x32_tiles.log; the next tile's old values prefetched spilled: 587-593 ms)
         const int lr = lane & 15, lk = lane >> 4;
-        for (int st = wave; st < nst; st += TH / 64) {
-          int I64 = 0;
-          while ((I64 + 1) * (I64 + 2) <= st) ++I64;
-          const int J32 = st - I64 * (I64 + 1);
-          const int ri0 = kb + 64 * I64, rj0 = kb + 32 * J32;
-          if (32 * J32 >= m) continue;
-          auto live = [&](int bi, int bj) {  // the block has a stored element (row >= column, both < rows)
-            return ri0 + 16 * bi < rows && rj0 + 16 * bj < rows && rj0 + 16 * bj <= ri0 + 16 * bi + 15;
-          };
-          double old[4][2][4];
+        const int T32 = (m + 31) / 32, nst32 = T32 * (T32 + 1) / 2;
+        auto tile_at = [&](int st, int& ri0, int& rj0) {  // st -> (I, J), J <= I
+          int I = 0;
+          while ((I + 1) * (I + 2) / 2 <= st) ++I;
+          ri0 = kb + 32 * I, rj0 = kb + 32 * (st - I * (I + 1) / 2);
+        };
+        auto load_old = [&](int ri0, int rj0, double (&o)[2][2][4]) {
 #pragma unroll
-          for (int bi = 0; bi < 4; ++bi)
+          for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
             for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
               for (int g = 0; g < 4; ++g) {
                 const int rr = min(ri0 + 16 * bi + lk + 4 * g, rows - 1), cc = rj0 + 16 * bj + lr;
-                old[bi][bj][g] = M[at(k0 + rr, k0 + min(cc, rr))];  // clamped into the stored lower triangle
+                o[bi][bj][g] = M[at(k0 + rr, k0 + min(cc, rr))];  // clamped into the stored lower triangle
               }
-          if (!GP && k0 == 0)  // first touch: A -> S (the clamped elements are never stored)
+        };
+        for (int st = wave; st < nst32; st += TH / 64) {
+          int ri0 = 0, rj0 = 0;
+          tile_at(st, ri0, rj0);
+          double oa[2][2][4];
+          load_old(ri0, rj0, oa);
+          auto live = [&](int bi, int bj) {  // the block has a stored element (row >= column, both < rows)
+            return ri0 + 16 * bi < rows && rj0 + 16 * bj < rows && rj0 + 16 * bj <= ri0 + 16 * bi + 15;
+          };
+          dx4 acc[2][2];
 #pragma unroll
-            for (int bi = 0; bi < 4; ++bi)
-#pragma unroll
-              for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                  const int rr = min(ri0 + 16 * bi + lk + 4 * g, rows - 1), cc = rj0 + 16 * bj + lr;
-                  old[bi][bj][g] = s_of(rr, min(cc, rr), old[bi][bj][g]);
-                }
-          dx4 acc[4][2];
-#pragma unroll
-          for (int bi = 0; bi < 4; ++bi)
+          for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
             for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = dx4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int q = 0; q < NB; q += 4) {  // (kb = NB whenever there are trailing rows)
-            double a[4], b[2];
+            double a[2], b[2];
 #pragma unroll
-            for (int bi = 0; bi < 4; ++bi) a[bi] = PAN(min(ri0 + 16 * bi + lr, rows - 1), q + lk);
+            for (int bi = 0; bi < 2; ++bi) a[bi] = PAN(min(ri0 + 16 * bi + lr, rows - 1), q + lk);
 #pragma unroll
             for (int bj = 0; bj < 2; ++bj) b[bj] = PAN(min(rj0 + 16 * bj + lr, rows - 1), q + lk);
 #pragma unroll
-            for (int bi = 0; bi < 4; ++bi)
+            for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
               for (int bj = 0; bj < 2; ++bj)
                 if (live(bi, bj)) acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[bi], b[bj], acc[bi][bj], 0, 0, 0);
           }
 #pragma unroll
-          for (int bi = 0; bi < 4; ++bi)
+          for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
             for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
               for (int g = 0; g < 4; ++g) {
                 const int r = ri0 + 16 * bi + lk + 4 * g, c = rj0 + 16 * bj + lr;
-                if (r < rows && c <= r) M[at(k0 + r, k0 + c)] = old[bi][bj][g] - acc[bi][bj][g];
+                double o = oa[bi][bj][g];
+                if (!GP && k0 == 0) {  // first touch: A -> S (the clamped elements are never stored)
+                  const int rr = min(r, rows - 1);
+                  o = s_of(rr, min(c, rr), o);
+                }
+                if (r < rows && c <= r) M[at(k0 + r, k0 + c)] = o - acc[bi][bj][g];
               }
         }
       } else {
