@@ -98,12 +98,14 @@ __device__ __forceinline__ void h16_store(float* __restrict__ dst, int64_t P, in
 }
 
 // CB: 16-pixel groups whose reads and MFMAs are batched per step (AUTO 4; 1 one group at a time)
-// PROBE (not reachable from the C ABI; tools/probe/h16_probe.hip): 5 / 6 = as 1 with the transposed reads and
-// MFMAs dropped / with those and the LDS parking dropped (the load pipeline alone); 1 = the coefficient stores dropped, 2 = the
-// stores non-temporal, 3 / 4 = (PTM-6, 1024-pixel tiles) each wave's 128 finished pixel rows staged in the free
-// half of the LDS tile and written back as three whole 1-KiB stores, plain / non-temporal
-// W: waves per workgroup (8; 16 with the 2048-pixel tile = 2-KiB runs per plane and wave, measurement)
-template <int K, int LAYOUT, int R, int STEP, int CB = 1, int PROBE = 0, int W = H16_W>
+// PROBE (not reachable from the C ABI; tools/probe/h16_probe.hip): 1 = the coefficient stores dropped, 2 = the
+// per-lane stores non-temporal, 5 / 6 = as 1 with the transposed reads and MFMAs dropped / with those and the
+// LDS parking dropped (the load pipeline alone)
+// W: waves per workgroup (8; 16 with the 2048-pixel tile = 2-KiB runs per plane and wave)
+// SM (PTM-6, pixel-major, 1024-pixel tiles on 8 waves): 0 per-lane coefficient stores, 1 / 2 each wave's 128
+// finished rows staged in the free half of the LDS tile and written back as three whole 1-KiB lines, plain /
+// non-temporal (2: AUTO since r05)
+template <int K, int LAYOUT, int R, int STEP, int CB = 1, int PROBE = 0, int W = H16_W, int SM = 0>
 __global__ void __launch_bounds__(64 * W)
 fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __restrict__ I, int64_t pb, int64_t pe,
         int tpw, int64_t P, int64_t lstride, int64_t cstride, float* __restrict__ coef, int64_t ocstride) {
@@ -230,7 +232,7 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
   // staged form (PROBE 3 / 4): the wave's 128 rows of 6 coefficients (3 KiB) parked in its slice of the free tile
   // buffer fb, read back as 16-B chunks 16·lane + 1 KiB·j and written as whole lines; the caller's barrier keeps
   // the other waves from parking into fb before every wave has read its slice back
-  constexpr bool STG = (PROBE == 3 || PROBE == 4) && K == 6 && R == 1024 && LAYOUT == RTI_COEF_PIXEL_MAJOR;
+  constexpr bool STG = SM != 0 && K == 6 && R == 1024 && W == 8 && LAYOUT == RTI_COEF_PIXEL_MAJOR && PROBE == 0;
   auto finish_staged = [&](int ti, int fb) {
     const int64_t w0 = tile_px(ti) + TL::WPX * wave;  // the wave's first pixel (1-KiB aligned rows)
     float* slice = reinterpret_cast<float*>(tile + fb * (STEP * TL::RS)) + wave * (TL::WPX * 6);
@@ -254,7 +256,7 @@ fit_h16(const unsigned char* __restrict__ op, int N, const unsigned char* __rest
       const floatx4 v = *reinterpret_cast<const floatx4*>(slice + f);
       float* d = dst + w0 * 6 + f;
       if (w0 + (f + 3) / 6 < pe) {
-        if constexpr (PROBE == 4)
+        if constexpr (SM == 2)
           __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(d));
         else
           *reinterpret_cast<floatx4*>(d) = v;
@@ -316,9 +318,13 @@ int launch_h16_t(const unsigned char* op, int N, const unsigned char* I, int64_t
     return fail(RTI_ERR_UNSUPPORTED, "rti_fit_shared_h16: LDS of %zu B (N=%d) exceeds 160 KiB", lds, N);
   // AUTO batches 4 groups per read/MFMA round (c2 u8 0.0379 against 0.0443 ms one group at a time, c3 / c4 u8
   // within 1 %: profiles/r04z_h16_batch_sweep_c*.log); RTI_KERNEL_TILE_DEPTH(1|8) for measurement
-  auto kern = cb == 8   ? fit_h16<K, LAYOUT, R, STEP, 8, 0, W>
-              : cb == 1 ? fit_h16<K, LAYOUT, R, STEP, 1, 0, W>
-                        : fit_h16<K, LAYOUT, R, STEP, 4, 0, W>;
+  // PTM-6 pixel-major on 1024-pixel tiles: staged whole-line non-temporal coefficient stores (r05; c3 u8
+  // 0.1833 vs 0.2148 ms, 0.1871 vs 0.1894 and 0.1909 vs 0.1899 on three boxes, bit-identical:
+  // profiles/r05am_*, r05af_*, r05j_*)
+  constexpr int SM = (K == 6 && R == 1024 && W == 8 && LAYOUT == RTI_COEF_PIXEL_MAJOR) ? 2 : 0;
+  auto kern = cb == 8   ? fit_h16<K, LAYOUT, R, STEP, 8, 0, W, SM>
+              : cb == 1 ? fit_h16<K, LAYOUT, R, STEP, 1, 0, W, SM>
+                        : fit_h16<K, LAYOUT, R, STEP, 4, 0, W, SM>;
   if (reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess)
     return fail(RTI_ERR_HIP, "rti_fit_shared_h16: cannot reserve %zu B of LDS", lds);
   const int64_t tiles = (P + R - 1) / R;

@@ -32,12 +32,12 @@ hipError_t reserve_lds(const void* kern, size_t bytes) {
 }
 }  // namespace rti
 
-template <int K, int PROBE>
+template <int K, int PROBE, int SM = 0>
 static int probe_t(const unsigned char* op, int N, const unsigned char* I, int64_t P, float* coef, hipStream_t s) {
   using namespace rti;
   constexpr int R = K <= 9 ? 1024 : 2048, STEP = 32;
   const size_t lds = h16_lds_bytes<R, STEP>(N);
-  auto kern = fit_h16<K, RTI_COEF_PIXEL_MAJOR, R, STEP, 4, PROBE>;
+  auto kern = fit_h16<K, RTI_COEF_PIXEL_MAJOR, R, STEP, 4, PROBE, H16_W, SM>;
   if (reserve_lds(reinterpret_cast<const void*>(kern), lds) != hipSuccess) return RTI_ERR_HIP;
   const int64_t tiles = (P + R - 1) / R, wpc = (int64_t)device_cus() * (2048 / R);
   const int tpw = (int)((tiles + wpc - 1) / wpc);
@@ -53,8 +53,8 @@ extern "C" int h16_probe(const void* op, int k, int N, const void* I, int64_t P,
   if (k == 6) switch (mode) {
       case 1: return probe_t<6, 1>(o, N, x, P, coef, s);
       case 2: return probe_t<6, 2>(o, N, x, P, coef, s);
-      case 3: return probe_t<6, 3>(o, N, x, P, coef, s);
-      case 4: return probe_t<6, 4>(o, N, x, P, coef, s);
+      case 3: return probe_t<6, 0, 1>(o, N, x, P, coef, s);
+      case 4: return probe_t<6, 0, 2>(o, N, x, P, coef, s);
       case 5: return probe_t<6, 5>(o, N, x, P, coef, s);
       case 6: return probe_t<6, 6>(o, N, x, P, coef, s);
       default: return probe_t<6, 0>(o, N, x, P, coef, s);

@@ -59,7 +59,7 @@ def main():
             st = plib.h16_probe(vp(op.data_ptr()), k, N, vp(I8.data_ptr()), ctypes.c_int64(P), vp(coef.data_ptr()),
                                 mode, vp(torch.cuda.current_stream(dev).cuda_stream))
             assert st == 0, st
-        variants.append(("probe_h16_same", lambda: pr(0)))
+        variants.append(("probe_h16_perlane", lambda: pr(0)))  # the r04 per-lane coefficient stores
         variants.append(("probe_h16_nostores", lambda: pr(1)))
         variants.append(("probe_h16_nt_stores", lambda: pr(2)))
         if k == 6:
