@@ -416,6 +416,23 @@ class FitWorkload(Workload):
                 f"oracle fit_shared_f32 (fp64 pinv + fp32 NumPy matmul, channel 0) on {rows}x{self.W} px x {self.N} "
                 f"lights")
 
+    def cpu_ref_fn(self):
+        """The reference's OWN least-squares path, not the port: every pixel builds its N x k design matrix
+        from its light list (analysis.py:280-291, float32 monomials with powf squares) and solves it with a
+        full fp64 SVD and no rcond (analysis.py:293-298), as interpolate_intensities calls it per pixel
+        (analysis.py:350-359); here batched (oracle.fit_perpixel) on the first rows of the same stack with the
+        shared directions broadcast to every pixel."""
+        o = oracle()
+        rows = max(1, min(self.ctx.h, 8))
+        npx = rows * self.W
+        sample = (self.I[0, :npx, :] if self.stack == "pixel" else self.I[0, :, :npx].T).float()
+        sample = np.ascontiguousarray(sample.cpu().numpy())
+        lu = np.broadcast_to(self.lu[None, :], (npx, self.N))
+        lv = np.broadcast_to(self.lv[None, :], (npx, self.N))
+        return (lambda: o.fit_perpixel(lu, lv, sample, self.basis), self.N * npx,
+                f"oracle fit_perpixel (per-pixel design matrix + batched fp64 NumPy SVD, no rcond: the reference's "
+                f"analysis.py:280-298 semantics, channel 0) on {rows}x{self.W} px x {self.N} lights")
+
 
 class FitResidualWorkload(FitWorkload):
     """One step = one rti_fit_shared_residual_svd call (what rti.fit_with_residual runs): coefficients +
@@ -939,11 +956,26 @@ def cpu_baseline(wl, budget_s):
         rate_n, reps_n = time_cpu(fn, units, budget_s / 2)
     with threadpool_limits(1):
         rate_1, reps_1 = time_cpu(fn, units, budget_s / 2)
-    return {"value": round(rate_n, 3), "unit": wl.unit, "cores": threads, "kind": "port",
-            "value_1thread": round(rate_1, 3),
-            "sample": f"{desc}; median of {reps_n} runs at {threads} BLAS threads (sched_getaffinity {aff}"
-                      f"{f', cgroup quota {quota}' if quota else ''}) and of {reps_1} runs at 1 thread, after 1 "
+    out = {"value": round(rate_n, 3), "unit": wl.unit, "cores": threads, "kind": "port",
+           "value_1thread": round(rate_1, 3),
+           "sample": f"{desc}; median of {reps_n} runs at {threads} BLAS threads (sched_getaffinity {aff}"
+                     f"{f', cgroup quota {quota}' if quota else ''}) and of {reps_1} runs at 1 thread, after 1 "
+                     f"warm-up each; {cpu_model()}"}
+    ref = getattr(wl, "cpu_ref_fn", None)
+    if ref is not None:  # the reference's own per-pixel SVD semantics, beside the port
+        fn, units, desc = ref()
+        with threadpool_limits(threads):
+            rr_n, rn = time_cpu(fn, units, budget_s / 4)
+        with threadpool_limits(1):
+            rr_1, r1 = time_cpu(fn, units, budget_s / 4)
+        out["reference_semantics"] = {
+            "value": round(rr_n, 3), "unit": wl.unit, "cores": threads, "value_1thread": round(rr_1, 3),
+            "kind": "reference-semantics port",
+            "sample": f"{desc}; median of {rn} runs at {threads} BLAS threads and of {r1} runs at 1 thread, after 1 "
                       f"warm-up each; {cpu_model()}"}
+        out["note"] = ("value = the build's vectorised port (one shared fp64 pinv, fp32 matmul); "
+                       "reference_semantics = the reference's per-pixel SVD least squares (analysis.py:280-298)")
+    return out
 
 
 # ---- multi-GPU legs ---------------------------------------------------------------------------
@@ -1117,7 +1149,8 @@ def main():
         raise SystemExit("--stack pixel applies to the fit configs (c2, c3, c4)")
     if args.kernel in ("q8", "h16") and (kind not in ("fit",) or args.in_dtype != "u8"):
         raise SystemExit(f"--kernel {args.kernel} is the 8-bit fit: it needs a fit config and --in-dtype u8")
-    if args.steps is None:
+    auto_steps = args.steps is None
+    if auto_steps:
         args.steps = DEFAULT_STEPS[kind]
 
     import torch
@@ -1157,9 +1190,18 @@ def main():
     wl = WORKLOADS[kind](args, cfg, ctx)
     torch.cuda.synchronize(dev)
 
+    tw = time.perf_counter()
     for i in range(args.warmup):
         wl.step(i)
     torch.cuda.synchronize(dev)
+    if auto_steps and args.warmup > 1:
+        # no --steps: enough steps for a timed region of >= 50 ms, so short kernels (u8, c2: 0.03-0.2 ms) are not
+        # dominated by the region's first launch and last sync (same count on every rank: the max is taken)
+        est = (time.perf_counter() - tw) / args.warmup
+        want = int(np.ceil(0.05 / max(est, 1e-6)))
+        if world > 1:
+            want = int(reduce_max([float(want)], ctx, backend)[0])
+        args.steps = max(args.steps, min(want, 5000))
 
     stream = torch.cuda.current_stream(dev)
     # timed region: exactly K steps between barrier + synchronize, nothing else enqueued
@@ -1245,6 +1287,10 @@ def main():
             "dtype": wl.dtype,
             "data": "synthetic (seeded smooth PTM/HSH coefficient fields + N(0,2) noise, rounded to 0..255, fp32)",
             "config": conf,
+            # the same work over the event-timed kernel time (median of 50 windows of >= 1 ms): a timed region of
+            # K short steps carries the launch/sync overhead of its first and last step, this figure does not
+            "value_kernel": round(wl.total_units / (kernel_ms * 1e-3) / 1e6, 1),
+            "timed_region_ms": round(elapsed * 1e3, 3),
             "roofline": wl.roofline(kernel_ms),
             "kernel_ms_stats": {"median": round(kernel_ms, 5), "min": round(float(wms.min()), 5),
                                 "mean": round(float(wms.mean()), 5), "n": 50, "launches_per_window": m,

@@ -349,7 +349,9 @@ int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp,
  * Device memory: the call allocates (stream-ordered, hipMallocAsync) and frees a workspace of
  * P·N·(8 + 8) bytes (weights + nodes) plus, for N > 256, one Cholesky slot of ≈ 4·(N+pad)² bytes (the packed
  * lower triangle) per workgroup on min(P, CUs) workgroups (≈ 3.3 GB at N = 1800, 6.7 GB at N = 2556, 17 GB at
- * N = 4089 on 256 CUs; above 4089 as many slots as 48 GiB holds, at least one), or for 139 <= N <= 256 an fp64
+ * N = 4089 on 256 CUs; above 4089 as many slots as fit in min(48 GiB, 90 % of the device's free memory less the
+ * weights and nodes), halved again while the allocation fails, at least one; the environment variable
+ * RTI_RBF_GP_WS_BYTES lowers that budget), or for 139 <= N <= 256 an fp64
  * fallback slot of 8·N·(N+1) bytes per CU (below: in LDS),
  * plus a P + 1 int list of the fallback's pixels; RTI_ERR_HIP if it cannot. */
 int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
@@ -361,6 +363,9 @@ int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dty
 int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                         const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
                         int* fallback_px, rti_stream_t stream);
+/* Cholesky workgroups (= workspace slots) of this thread's most recent rti_rbf_perpixel call (N > 256), 0 for
+ * the other solvers.  For tests and timing tools; the results do not depend on it. */
+int64_t rti_rbf_last_chol_grid(void);
 
 /* ---- device: light vectors ---------------------------------------------------------
  * The light-vector half of compute_intensities (analysis.py:221-231) for an

@@ -955,8 +955,28 @@ __host__ __device__ constexpr int64_t chol_slot_doubles(int N) { return chol_mat
 // GP form (N > RBF_CH_MAX_N): + y1, y2 and the nodes (two float rows) in the slot
 __host__ __device__ constexpr int64_t chol_slot_doubles_gp(int N) { return chol_slot_doubles(N) + 3 * chol_ld(N); }
 constexpr int RBF_CH_GP_NB = 32;  // GP panel width (only its diagonal block is in LDS)
-constexpr int RBF_GP_MAX_N = 32768;  // a 4.3 GB slot per workgroup (the grid shrinks to fit RBF_GP_WS_BYTES)
+constexpr int RBF_GP_MAX_N = 32768;  // a 4.3 GB slot per workgroup (the grid shrinks to fit gp_ws_budget)
 constexpr size_t RBF_GP_WS_BYTES = (size_t)48 << 30;
+
+// GP slot budget: at most RBF_GP_WS_BYTES, and at most 90 % of the device's free memory less the node-major
+// weights and nodes (`other` bytes) allocated with the slots; RTI_RBF_GP_WS_BYTES (environment, read per call)
+// lowers it (tests force a one-slot grid).  The grid is at least one slot whatever the budget.
+size_t gp_ws_budget(size_t other) {
+  size_t budget = RBF_GP_WS_BYTES;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+    const size_t usable = free_b / 10 * 9;
+    budget = usable > other ? (usable - other < budget ? usable - other : budget) : 0;
+  } else {
+    (void)hipGetLastError();
+  }
+  if (const char* e = getenv("RTI_RBF_GP_WS_BYTES")) {
+    const long long v = atoll(e);
+    if (v >= 0 && (size_t)v < budget) budget = (size_t)v;
+  }
+  return budget;
+}
+thread_local int64_t rbf_last_chol_grid_v = 0;  // slots (= Cholesky workgroups) of the last rti_rbf_perpixel call
 
 // Phase timer for tools/probe/chol_probe.hip (compiled in only there): per workgroup, the steady-clock
 // ticks spent in each phase, summed over its pixels (a barrier closes every phase).
@@ -1081,24 +1101,24 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
       double* colp = rowp + (size_t)ntl * 64;     // [ntl][64]
       double* rbuf = colp + (size_t)ntl * 64 + wave * (8 * 64);  // [8][64] per wave
       for (int st = wave; st < ntl; st += TH / 64) {
-        int I = 0;
-        while ((I + 1) * (I + 2) / 2 <= st) ++I;
-        const int J = st - I * (I + 1) / 2;
-        const int j = 64 * J + lane;
+        int tI = 0;
+        while ((tI + 1) * (tI + 2) / 2 <= st) ++tI;
+        const int tJ = st - tI * (tI + 1) / 2;
+        const int j = 64 * tJ + lane;
         const bool jv = j < N;
         const double xj = (double)xs[jv ? j : 0], yj = (double)ys[jv ? j : 0];
         double cacc = 0.0;
-        const int rows_t = min(64, N - 64 * I);
+        const int rows_t = min(64, N - 64 * tI);
         for (int m0 = 0; m0 < rows_t; m0 += 8) {
           double v[8];
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const int i = 64 * I + m0 + q;
+            const int i = 64 * tI + m0 + q;
             const bool iv = i < N;
             const double d = dist64((double)xs[iv ? i : 0], (double)ys[iv ? i : 0], xj, yj);
             const double dd = iv && jv ? d : 0.0;
             v[q] = dd;
-            if (I > J) cacc += dd;
+            if (tI > tJ) cacc += dd;
             dup = dup || (iv && jv && j != i && d == 0.0);
             if (iv && jv && j <= i && i < n) M[at(i, j)] = d;  // raw A, turned into S on its first read
           }
@@ -1119,14 +1139,14 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (I > J) colp[(size_t)st * 64 + lane] = cacc;
+        if (tI > tJ) colp[(size_t)st * 64 + lane] = cacc;
       }
       __syncthreads();
       for (int i = t; i < N; i += TH) {  // row i: its row-block's row partials, then the column partials below
-        const int I = i >> 6, r = i & 63;
+        const int tI = i >> 6, r = i & 63;
         double rs = 0.0;
-        for (int J = 0; J <= I; ++J) rs += rowp[(size_t)(I * (I + 1) / 2 + J) * 64 + r];
-        for (int I2 = I + 1; I2 < T64r; ++I2) rs += colp[(size_t)(I2 * (I2 + 1) / 2 + I) * 64 + r];
+        for (int tJ = 0; tJ <= tI; ++tJ) rs += rowp[(size_t)(tI * (tI + 1) / 2 + tJ) * 64 + r];
+        for (int I2 = tI + 1; I2 < T64r; ++I2) rs += colp[(size_t)(I2 * (I2 + 1) / 2 + tI) * 64 + r];
         gv[i] = fma(e, rs, -(i < n ? dist(n, i) : 0.0));
       }
     } else {
@@ -1310,9 +1330,9 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
         const int lr = lane & 15, lk = lane >> 4;
         const int T32 = (m + 31) / 32, nst32 = T32 * (T32 + 1) / 2;
         auto tile_at = [&](int st, int& ri0, int& rj0) {  // st -> (I, J), J <= I
-          int I = 0;
-          while ((I + 1) * (I + 2) / 2 <= st) ++I;
-          ri0 = kb + 32 * I, rj0 = kb + 32 * (st - I * (I + 1) / 2);
+          int tI = 0;
+          while ((tI + 1) * (tI + 2) / 2 <= st) ++tI;
+          ri0 = kb + 32 * tI, rj0 = kb + 32 * (st - tI * (tI + 1) / 2);
         };
         auto load_old = [&](int ri0, int rj0, double (&o)[2][2][4]) {
 #pragma unroll
@@ -1586,6 +1606,8 @@ void launch_eval(int ol, const double* wT, const float2* xyT, int N, int64_t P, 
 using namespace rti;
 
 
+extern "C" int64_t rti_rbf_last_chol_grid(void) { return rbf_last_chol_grid_v; }
+
 extern "C" int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                                 const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
                                 rti_stream_t stream) {
@@ -1616,21 +1638,31 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
   int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
   const int64_t slot_doubles = N > RBF_CH_MAX_N ? chol_slot_doubles_gp(N) : chol_slot_doubles(N);
-  if (chol && N > RBF_CH_MAX_N) {  // GP slots (≈ 4·N² bytes each): as many workgroups as RBF_GP_WS_BYTES holds
-    const int64_t fit = (int64_t)(RBF_GP_WS_BYTES / ((size_t)slot_doubles * sizeof(double)));
+  const size_t node_bytes = (size_t)N * P * (sizeof(double) + sizeof(float2));
+  if (chol && N > RBF_CH_MAX_N) {  // GP slots (≈ 4·N² bytes each): as many workgroups as the budget holds
+    const int64_t fit = (int64_t)(gp_ws_budget(node_bytes) / ((size_t)slot_doubles * sizeof(double)));
     chol_grid = fit < 1 ? 1 : (fit < chol_grid ? fit : chol_grid);
   }
   const int64_t fb_grid = fb ? (P < device_cus() ? P : device_cus()) : 0;
   const size_t fb_ws_bytes = fb ? (fb_in_lds(N) ? 0 : (size_t)fb_grid * N * (N + 1) * sizeof(double))
                                 : (chol ? (size_t)chol_grid * slot_doubles * sizeof(double) : 0);
   const size_t flag_bytes = fb ? ((size_t)(P + 1) * sizeof(int) + 255) / 256 * 256 : 0;  // count + pixel list
-  const size_t bytes = (size_t)N * P * (sizeof(double) + sizeof(float2)) + fb_ws_bytes + flag_bytes;
-  if (hipMallocAsync(&ws, bytes, s) != hipSuccess)
-    return fail(RTI_ERR_HIP, "rti_rbf_perpixel: workspace allocation of %zu bytes failed", bytes);
+  size_t fb_ws_bytes_v = fb_ws_bytes;
+  size_t bytes = node_bytes + fb_ws_bytes_v + flag_bytes;
+  while (hipMallocAsync(&ws, bytes, s) != hipSuccess) {
+    // the GP path strides over the pixels from any number of slots: retry with half as many before failing
+    if (!(chol && N > RBF_CH_MAX_N && chol_grid > 1))
+      return fail(RTI_ERR_HIP, "rti_rbf_perpixel: workspace allocation of %zu bytes failed", bytes);
+    (void)hipGetLastError();
+    chol_grid = (chol_grid + 1) / 2;
+    fb_ws_bytes_v = (size_t)chol_grid * slot_doubles * sizeof(double);
+    bytes = node_bytes + fb_ws_bytes_v + flag_bytes;
+  }
+  rbf_last_chol_grid_v = chol ? chol_grid : 0;
   double* wT = static_cast<double*>(ws);
   float2* xyT = reinterpret_cast<float2*>(wT + (size_t)N * P);
   double* fb_ws = reinterpret_cast<double*>(xyT + (size_t)N * P);
-  int* redo = reinterpret_cast<int*>(reinterpret_cast<char*>(fb_ws) + fb_ws_bytes);
+  int* redo = reinterpret_cast<int*>(reinterpret_cast<char*>(fb_ws) + fb_ws_bytes_v);
   if (fb && hipMemsetAsync(redo, 0, sizeof(int), s) != hipSuccess) {
     (void)hipFreeAsync(ws, s);
     return fail(RTI_ERR_HIP, "rti_rbf_perpixel: clearing the fallback count failed");

@@ -79,6 +79,7 @@ SIGNATURES = {
     "rti_status_string": (ctypes.c_char_p, [_c_int]),
     "rti_last_error": (ctypes.c_char_p, []),
     "rti_last_launch_count": (ctypes.c_int, []),
+    "rti_rbf_last_chol_grid": (_c_i64, []),
     "rti_basis_terms": (_c_int, [_c_int]),
     "rti_device_count": (_c_int, []),
     "rti_design_matrix": (_c_int, [_c_int, _c_float_p, _c_float_p, _c_int, _c_double_p]),

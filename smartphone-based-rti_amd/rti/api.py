@@ -192,8 +192,9 @@ _PM_KERNELS = ("auto", "valu", "mfma", "tile")  # the selectors rti_fit_shared_p
 
 
 def _fit_shared_pixel_major(I, lu, lv, b, k, rcond, cl, kernel, given_pixel_major):
-    """rti.fit(mode="shared") on a pixel-major stack: ``rti_fit_shared_pm`` on the tensor's own memory."""
-    if kernel not in _PM_KERNELS:
+    """rti.fit(mode="shared") on a pixel-major stack: ``rti_fit_shared_pm`` on the tensor's own memory.
+    Integer kernel words pass through unchanged (the C entry refuses bits it does not document)."""
+    if isinstance(kernel, str) and kernel not in _PM_KERNELS:
         raise NotImplementedError(f"kernel={kernel!r} does not take pixel-major stacks (rti_fit_shared_pm: "
                                   f"{', '.join(_PM_KERNELS)}); pass stack='light' with a light-major stack")
     if given_pixel_major:
@@ -296,8 +297,7 @@ def fit_shared_pm_into(pinv_dev, I, coef, *, k, layout="pixel", kernel="auto", f
         I3 = I3.contiguous()
     ps = I3.stride(1) if P > 1 else N
     cs = I3.stride(0) if C > 1 else P * ps
-    kern = _KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
-    kern = (kern & 0xff) | int(flags)
+    kern = (_KERNELS[kernel] if isinstance(kernel, str) else int(kernel)) | int(flags)
     st = L.lib().rti_fit_shared_pm(_vp(pinv_dev), k, N, _vp(I3), _IN_DTYPES[I.dtype], P, C, ps, cs, _vp(coef),
                                    _layout_id(layout), P * k, kern, _stream_of(I))
     L.check(st, "rti_fit_shared_pm")

@@ -92,7 +92,7 @@ def fit_rowtiled(I_rows, lu, lv, H, basis="ptm", rcond=None, gather=True, group=
 
 
 def gather_rows_pipelined(produce, h_local, H, trail, dtype, device, chunks=4, group=None, partition="block",
-                          out=None, channels=None):
+                          out=None, channels=None, staging=None):
     """All-gather a row-tiled map while it is being produced (overlap the coefficient
     all-gather with fitting).
 
@@ -109,6 +109,8 @@ def gather_rows_pipelined(produce, h_local, H, trail, dtype, device, chunks=4, g
     every chunk is gathered straight into its place in the [H, *trail] map.
     partition="block": local rows = row_range(H, G, r); with G | H and chunks | H/G each chunk is
     gathered into a staging buffer and moved into place by one strided copy; other shapes pad.
+    staging: a dict the caller keeps across calls (RowTiledFitter does); the block partition's staging and
+    pad buffers live there, so only the first call allocates.
     Returns the full [H, *trail] (or [C, H, *trail]) map."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -154,20 +156,33 @@ def gather_rows_pipelined(produce, h_local, H, trail, dtype, device, chunks=4, g
     chunks = max(1, min(chunks, hmax))
     even = H % world == 0 and (H // world) % chunks == 0
     cmax = -(-hmax // chunks)
+
+    def staged(key, shape, zero=False):
+        """A device buffer for this call's chunk `key`: from `staging` (allocated on its first call, reused
+        after: the previous call's copies out of it are ordered before this call's collective on the stream)."""
+        if staging is None:
+            return (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=device)
+        buf = staging.get(key)
+        if buf is None or tuple(buf.shape) != tuple(shape) or buf.dtype != dtype:
+            buf = staging[key] = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=device)
+        elif zero:
+            buf.zero_()
+        return buf
+
     pending = []
     for j in range(chunks):
         c0, c1 = row_range(h_local, chunks, j)
         if even:
             pcs = parts_of(produce(c0, c1))
         else:
-            pad = torch.zeros(lead + (cmax,) + trail, dtype=dtype, device=device)
+            pad = staged(("pad", j), lead + (cmax,) + trail, zero=True)
             if c1 > c0:
                 pad.narrow(len(lead), 0, c1 - c0).copy_(produce(c0, c1))
             pcs = parts_of(pad)
         for c, part in enumerate(pcs):
             part = part.contiguous()
             if nccl:
-                buf = torch.empty((world,) + tuple(part.shape), dtype=dtype, device=device)
+                buf = staged(("gather", c, j), (world,) + tuple(part.shape))
                 pending.append((c, j, dist.all_gather_into_tensor(buf.view((-1,) + trail), part, group=group,
                                                                   async_op=True), buf))
             else:
@@ -262,18 +277,35 @@ class RowTiledFitter:
             if pv.shape[1] != self.N:
                 raise ValueError(f"{pv.shape[1]} light directions for {self.N} intensity planes")
             self.pinv = torch.as_tensor(pv.astype(np.float32), device=dev)
-            self.kern = api._KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
             self.dtype = torch.float32
-            self.h16 = None
-            if (stack == "light" and self.I.dtype == torch.uint8 and kernel == "auto" and self.W % 16 == 0
-                    and self.k in (6, 9, 16) and self.N <= int(L.lib().rti_fit_shared_h16_max_lights())
-                    and np.isfinite(pv).all() and self.I.data_ptr() % 16 == 0):
-                self.h16 = torch.as_tensor(api.h16_operator(pv), device=dev)
+            # 8-bit matrix-core fits (rti.fit's AUTO for uint8 light-major stacks, or asked for by name): the
+            # split-fp16 operator (rti_fit_shared_h16) or the int8 fixed-point one (rti_fit_shared_q8)
+            self.u8, self.u8_op = None, None
+            mk = "h16" if kernel == "auto" else kernel
+            if isinstance(kernel, str) and kernel not in api._KERNELS and kernel not in ("h16", "q8"):
+                raise ValueError(f"unknown kernel {kernel!r}")
+            if mk in ("h16", "q8"):
+                maxn = (L.lib().rti_fit_shared_h16_max_lights if mk == "h16" else
+                        L.lib().rti_fit_shared_q8_max_lights)()
+                ok = (stack == "light" and self.I.dtype == torch.uint8 and self.W % 16 == 0 and self.k in (6, 9, 16)
+                      and self.N <= int(maxn) and np.isfinite(pv).all() and self.I.data_ptr() % 16 == 0)
+                if ok:
+                    self.u8 = mk
+                    self.u8_op = torch.as_tensor(api.h16_operator(pv) if mk == "h16" else api.q8_operator(pv),
+                                                 device=dev)
+                elif kernel in ("h16", "q8"):
+                    raise NotImplementedError(f"kernel={kernel!r} needs a light-major uint8 stack, W % 16 == 0, "
+                                              f"k in (6, 9, 16), N <= {int(maxn)} and a finite pseudo-inverse")
+            # every other selector (string or integer kernel word) goes to rti_fit_shared / rti_fit_shared_pm
+            # unchanged: the C entries refuse bits they do not document
+            self.kern = 0 if mk in ("h16", "q8") else (api._KERNELS[kernel] if isinstance(kernel, str)
+                                                       else int(kernel))
         self.dt = api._IN_DTYPES[self.I.dtype]
         self.coef = torch.empty((self.C, self.h, self.W, self.k), dtype=self.dtype, device=dev)
         lead = (self.C,) if self.C > 1 or self.I.dim() == 4 else ()
         self.full = torch.empty(lead + (H, self.W, self.k), dtype=self.dtype, device=dev)
         self.channels = self.C if lead else None
+        self._staging = {}  # block-partition gather/pad buffers, allocated by the first call only
 
     def _produce(self, c0, c1):
         W, k, N, C, h = self.W, self.k, self.N, self.C, self.h
@@ -292,12 +324,13 @@ class RowTiledFitter:
             L.check(st, "rti_fit_perpixel_cam")
         elif self.stack == "pixel":
             st = lib.rti_fit_shared_pm(api._vp(self.pinv), k, N, self.I.data_ptr() + c0 * W * N * es, self.dt, P, C,
-                                       N, h * W * N, dst, L.RTI_COEF_PIXEL_MAJOR, ocs, self.kern & 0xff, s)
+                                       N, h * W * N, dst, L.RTI_COEF_PIXEL_MAJOR, ocs, self.kern, s)
             L.check(st, "rti_fit_shared_pm")
-        elif self.h16 is not None:
-            st = lib.rti_fit_shared_h16(api._vp(self.h16), k, N, self.I.data_ptr() + c0 * W, P, C, h * W, N * h * W,
-                                        dst, L.RTI_COEF_PIXEL_MAJOR, ocs, 0, s)
-            L.check(st, "rti_fit_shared_h16")
+        elif self.u8 is not None:
+            fn = lib.rti_fit_shared_h16 if self.u8 == "h16" else lib.rti_fit_shared_q8
+            st = fn(api._vp(self.u8_op), k, N, self.I.data_ptr() + c0 * W, P, C, h * W, N * h * W,
+                    dst, L.RTI_COEF_PIXEL_MAJOR, ocs, 0, s)
+            L.check(st, f"rti_fit_shared_{self.u8}")
         else:
             st = lib.rti_fit_shared(api._vp(self.pinv), k, N, self.I.data_ptr() + c0 * W * es, self.dt, P, C, h * W,
                                     N * h * W, dst, L.RTI_COEF_PIXEL_MAJOR, ocs, self.kern, s)
@@ -307,7 +340,8 @@ class RowTiledFitter:
     def __call__(self):
         return gather_rows_pipelined(self._produce, self.h, self.H, (self.W, self.k), self.dtype,
                                      self.I.device, chunks=self.chunks, group=self.group,
-                                     partition=self.partition, out=self.full, channels=self.channels)
+                                     partition=self.partition, out=self.full, channels=self.channels,
+                                     staging=self._staging)
 
 
 def fit_rowtiled_overlapped(I_rows, lu=None, lv=None, H=None, basis="ptm", rcond=None, chunks=4, group=None,

@@ -217,6 +217,30 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     assert ok, err
 
 
+@pytest.mark.parametrize("budget_slots", [0, 2])
+def test_rbf_perpixel_gp_small_workspace_budget(cuda, monkeypatch, budget_slots):
+    """Above 4089 lights the Cholesky slots (≈ 4·N² bytes each) are sized from the device's free memory, not a
+    fixed 48 GiB: a budget below one slot still runs ONE workgroup striding over every pixel, and a budget of
+    two slots runs two (RTI_RBF_GP_WS_BYTES lowers the budget).  Same results as the oracle either way."""
+    n = 4090
+    ld = (n + 31) // 32 * 32
+    slot = 8 * ((ld * (ld + 1) // 2 + 31) // 32 * 32 + 6 * ld)  # chol_slot_doubles_gp(n) * 8 bytes
+    monkeypatch.setenv("RTI_RBF_GP_WS_BYTES", str(budget_slots * slot + slot // 2 if budget_slots else 1))
+    ys, xs = np.mgrid[0:1, 0:3]
+    rng = np.random.default_rng(77)
+    cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
+    lu, lv = o.light_dirs_for_pixels(cams, xs.ravel(), ys.ravel())
+    npx = xs.size
+    inten = rng.integers(0, 256, (npx, n)).astype(np.int32)
+    qu, qv = rng.uniform(-1, 1, 64), rng.uniform(-1, 1, 64)
+    out = rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv).cpu().numpy()
+    grid = int(rti._lib.lib().rti_rbf_last_chol_grid())
+    assert grid == max(1, min(budget_slots, npx)), grid
+    ref = np.stack([o.rbf_linear(lu[p], lv[p], inten[p], qu, qv) for p in range(npx)])
+    err, ok = relight_close(out, ref, rtol=1e-8)
+    assert ok, err
+
+
 @pytest.mark.parametrize("n", [81, 128, 129, 200, 256, 257, 400, 600, 4100])
 def test_rbf_perpixel_large_n_repeated_node_raises(cuda, n):
     """A repeated light direction makes A exactly singular: SciPy raises LinAlgError; so do the

@@ -82,7 +82,18 @@ def _pipelined_worker(rank, world, port, H, W, chunks, q):
 
         full = gather_rows_pipelined(produce, r1 - r0, H, (W, 6), torch.float32, torch.device("cpu"), chunks=chunks)
         covered = sorted(calls) == calls and sum(b - a for a, b in calls) == r1 - r0
-        q.put((rank, bool(torch.equal(full, full_ref)), covered))
+        ok = bool(torch.equal(full, full_ref))
+        # with a caller-kept staging dict the second call reuses the first call's buffers (no allocation)
+        staging = {}
+        for it in range(2):
+            out = gather_rows_pipelined(produce, r1 - r0, H, (W, 6), torch.float32, torch.device("cpu"),
+                                        chunks=chunks, staging=staging)
+            ok = ok and bool(torch.equal(out, full_ref))
+            ptrs = {k: v.data_ptr() for k, v in staging.items()}
+            if it == 0:
+                first = ptrs
+        ok = ok and ptrs == first
+        q.put((rank, ok, covered))
     finally:
         dist.destroy_process_group()
 
