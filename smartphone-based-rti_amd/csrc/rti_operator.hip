@@ -165,14 +165,23 @@ template <typename T, typename TO, bool VEC, bool NTS = true, int NBLK = 4>
 __global__ void __launch_bounds__(256)
 apply_op_f16s(const _Float16* ohi, const _Float16* olo, int Kp, float inv_s, int E, int N,
               const T* __restrict__ I, int64_t P, int64_t lstride, int64_t cstride, TO* __restrict__ out,
-              int64_t orow, int64_t ocs) {
+              int64_t orow, int64_t ocs, int xcd_order) {
   constexpr bool EXACT = std::is_same<T, uint8_t>::value;  // 0..255: exact in fp16, t = 1
   constexpr int TP = 32 * NBLK;  // pixels per workgroup tile
   extern __shared__ __attribute__((aligned(16))) _Float16 sI[];  // [2][TP][KPITCH]
   __shared__ float s_red[4];
   const int KPITCH = Kp + 8;  // 16-B pad between pixel rows
   _Float16* sIlo = sI + TP * KPITCH;
-  const int64_t p0 = (int64_t)blockIdx.x * TP;
+  // xcd_order (measurement, RTI_OP_XCD=1): workgroups are dispatched round-robin over the 8 XCDs, so workgroup b
+  // runs on XCD b % 8; this order gives each XCD one contiguous run of pixel tiles (its table writes stay in one
+  // run of every output row) instead of every eighth tile
+  int64_t tile = blockIdx.x;
+  if (xcd_order) {
+    const int64_t g = gridDim.x, per = (g + 7) / 8, x = blockIdx.x % 8, i = blockIdx.x / 8;
+    const int64_t full = g - 8 * (per - 1);  // XCDs holding `per` tiles (the others per - 1)
+    tile = x < full ? x * per + i : full * per + (x - full) * (per - 1) + i;
+  }
+  const int64_t p0 = tile * TP;
   const T* __restrict__ src = I + (int64_t)blockIdx.z * cstride;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
@@ -380,8 +389,9 @@ int launch_f16(const _Float16* hi, const _Float16* lo, int Kp, float inv_s, int 
       reserve_lds(reinterpret_cast<const void*>(k), lds) !=
           hipSuccess)
     return fail(RTI_ERR_HIP, "rti_apply_operator_f16: cannot reserve %zu B of LDS", lds);
+  const char* xo = getenv("RTI_OP_XCD");  // measurement
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, hi, lo, Kp, inv_s, E, N, static_cast<const T*>(I), P, ls, cs,
-                     static_cast<TO*>(out), orow, ocs);
+                     static_cast<TO*>(out), orow, ocs, xo ? atoi(xo) : 0);
   return check_launch("rti_apply_operator_f16");
 }
 

@@ -1494,6 +1494,539 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
 #endif
 }
 
+// ---- Left-looking tiled Cholesky on the fp64 matrix cores (r06; 256 < N <= RBF_LL_MAX_N) ------------------
+// The same bordered system as rbf_solve_chol (S = −(HAH)[:n, :n] = L Lᵀ, n = N − 1), factored LEFT-looking in block
+// columns of 64 with L kept in the slot in the matrix cores' own operand layout, so that every element of the
+// trailing matrix is formed ONCE (in registers) instead of being read and rewritten by every panel:
+//   * tile (rg, jg) = rows 16·rg .. +15, columns 4·jg .. +3 of L, 64 doubles in lane order l = row%16 + 16·(col%4):
+//     exactly what lane l supplies as the A or B operand of v_mfma_f64_16x16x4f64 (A[m][k] / B[k][n], m or n = l&15,
+//     k = l>>4), and what lane l holds in register g of a D tile whose rows are 4g + (l>>4) and columns l & 15 —
+//     so loads, MFMAs and stores are all whole 512-B tiles, coalesced, with no shuffles;
+//   * block column J (columns J0 .. J0 + 63): every wave owns up to 4 row groups (16 rows) per pass and holds
+//     Cᵀ[c][i] = Σ_q L[J0+c][q]·L[i][q] for them in 16 accumulator tiles; per earlier block column K the 64 rows
+//     J0 .. J0+63 of K (32 KB, the A operands, = the B operands of the diagonal row groups) are staged in LDS
+//     (double-buffered, the next chunk's loads in flight during this chunk's MFMAs) and the other row groups'
+//     B tiles stream from the slot.  Then C = S − Cᵀ with S formed from the node distances in registers (the
+//     slot never holds S or A);
+//   * the 64 columns are finished in 4 sub-panels of 16: sub-panel j is updated by the finished sub-panels k < j
+//     (MFMA, L_D(j,k) from LDS), its 16×16 diagonal block is factored AND inverted by one wave in registers (lane
+//     per row, readlane broadcasts, 16 steps), and every row group below multiplies by that inverse (4 MFMAs);
+//   * the right-hand sides c₁ and m ride along as two extra ROWS (n64, n64 + 1) of the matrix: their rows of L are
+//     L⁻¹c₁ and L⁻¹m, so the forward substitution is the factorization itself;
+//   * rows/columns n .. n64 − 1 are padded with the identity (the last block column runs unguarded).
+// The backward substitution Lᵀ z = y is a GEMV per block column over its tiles (coalesced) plus the 64×64
+// diagonal part from the 16×16 inverses; then the bordered elimination and w = H y as rbf_solve_chol.
+// Slot traffic per pixel at N = 400: ≈ 2.0 MB of B/A tiles read, 0.9 MB of L written, 0.9 MB read back by the
+// backward pass — against ≈ 8 MB for the right-looking panels (each panel re-read and re-wrote the trailing
+// triangle).  A non-positive pivot (repeated or nearly repeated nodes) reports RTI_ERR_SINGULAR like rbf_solve_chol.
+// 8 waves (two per SIMD, 256 registers each) of 4 row groups.  (4 waves of 8 row groups, 512 registers each with the
+// accumulators in AGPRs, spilled far more: 738 VGPRs)
+constexpr int RBF_LL_TH = 512;
+constexpr int RBF_LL_RGW = 4;  // row groups per wave per pass (16 accumulator tiles)
+constexpr int RBF_LL_MAX_N = 1022;
+__host__ __device__ constexpr int ll_n64(int N) { return (N - 1 + 63) / 64 * 64; }
+__host__ __device__ constexpr int ll_groups(int N) { return ll_n64(N) / 16 + 1; }  // + the right-hand-side group
+// (tiles / 16) of the block columns before K: block column K' holds row groups 4(K' + 1) .. G − 1
+__host__ __device__ constexpr int64_t ll_col_tiles(int G, int K) { return (int64_t)K * (G - 4) - 2 * (int64_t)K * (K - 1); }
+constexpr int LL_DIAG = 2560;  // per block column: 6 off-diagonal 16×16 blocks of L_D + 4 diagonal inverses
+__host__ __device__ constexpr int64_t ll_slot_doubles(int N) {
+  return ll_col_tiles(ll_groups(N), ll_n64(N) / 64) * 1024 + (int64_t)(ll_n64(N) / 64) * LL_DIAG;
+}
+// LDS: A chunks [2][4096], the block column's L_D blocks / inverses [2560], the leaf's two 16×17 matrices and pivots
+// (backward: 2×64 right-hand sides) [576], z [2][n64], g, c, m [np] each, the nodes [2][np] floats; np = n64 + 64 >= N, the entries past N
+// zero, so every column index j < n64 reads in bounds and the (many) per-column loads share one base address
+__host__ __device__ constexpr int ll_np(int N) { return ll_n64(N) + 64; }
+__host__ __device__ constexpr size_t ll_lds_bytes(int N) { return (size_t)(11328 + 2 * ll_n64(N) + 4 * ll_np(N)) * 8; }
+static_assert(ll_lds_bytes(RBF_LL_MAX_N) <= 160 * 1024 - 256, "RBF_LL_MAX_N");
+__host__ __device__ constexpr int ll_ls(int jp, int j) { return jp * (jp - 1) / 2 + j; }  // L_D block (jp, j), jp > j
+
+template <typename T>
+__global__ void __launch_bounds__(RBF_LL_TH)
+rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
+              double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status, double* __restrict__ ws) {
+  constexpr int TH = RBF_LL_TH, RGW = RBF_LL_RGW, NWV = TH / 64, PASS = NWV * RGW;  // PASS = 32 row groups
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  // wave index through readfirstlane: the compiler then knows every wave-dependent condition (row groups, diagonal
+  // sub-blocks) is uniform and branches on SCC instead of masking EXEC around the MFMAs
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane & 15, lk = lane >> 4;
+  const int n = N - 1, n64 = ll_n64(N), nbc = n64 / 64, G = n64 / 16 + 1;
+  double* slot = ws + (int64_t)blockIdx.x * ll_slot_doubles(N);
+  double* diagw = slot + ll_col_tiles(G, nbc) * 1024;  // [nbc][LL_DIAG]
+  double* Ab = smem;                                   // [2][4096]: A chunks, tiles [c-group][jl][64]
+  double* Dg = smem + 8192;                            // [10][4][64]: L_D(jp, j) (6), then the inverses (4)
+  double* lf = smem + 10752;                           // [576] the leaf; backward: [2][64] right-hand sides + [2][16]
+  double* zv = smem + 11328;                           // [2][n64]
+  const int np = ll_np(N);
+  double* gl = zv + 2 * n64;                           // g = A u
+  double* cvl = gl + np;                               // c = H b
+  double* mvl = cvl + np;                              // m = (HAH)[:, n]
+  float* xs = reinterpret_cast<float*>(mvl + np);
+  float* ys = xs + np;
+  __shared__ double red[TH / 64];
+  __shared__ int s_bad;
+  const double e = 1.0 / sqrt((double)N), beta = 1.0 / (1.0 - e);  // H = I − β u uᵀ, u = e·1 − e_n
+  auto u = [&](int j) { return j < n ? e : (j == n ? e - 1.0 : 0.0); };
+  auto sum_all = [&](double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < TH / 64; ++i) r += red[i];
+    return r;
+  };
+  auto dist = [&](int i, int j) { return dist64((double)xs[i], (double)ys[i], (double)xs[j], (double)ys[j]); };
+  // the slot's tile (rg, jg), rg >= 4·(jg/16 + 1)
+  auto tile = [&](int rg, int jg) -> double* {
+    const int K = jg >> 4;
+    return slot + ((ll_col_tiles(G, K) + (rg - 4 * (K + 1))) * 16 + (jg & 15)) * 64;
+  };
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+#ifdef RTI_CHOL_PROFILE
+  long long prof_[16] = {}, last_ = wall_clock64();
+#endif
+
+  for (int64_t p = blockIdx.x; p < P; p += gridDim.x) {
+    const int64_t base = p * N;
+    if (t == 0) s_bad = 0;
+    for (int j = t; j < np; j += TH) {
+      if (j < N) {
+        const float x = lu[base + j], y = lv[base + j];
+        xs[j] = x, ys[j] = y;
+        xyT[(int64_t)j * P + p] = make_float2(x, y);
+        zv[j] = ldd(I + base + j);  // b (zv is free until the backward pass)
+      } else {
+        xs[j] = 0.f, ys[j] = 0.f, gl[j] = 0.0, cvl[j] = 0.0, mvl[j] = 0.0;
+      }
+    }
+    __syncthreads();
+    CH_MARK(0);
+    // A's row sums and the repeated-node check (SciPy: LinAlgError).  Where its partials fit in the (still unused)
+    // chunk / diagonal / leaf LDS, the SYMMETRIC form of rbf_solve_chol: each distance of the lower triangle once, in
+    // 64×64 tiles (lane = column), column partials in registers, row partials through a per-wave LDS slice, every
+    // row's sum added up in a fixed order; otherwise RB rows per wave, every distance of a row
+    bool dup = false;
+    const int T64r = (N + 63) / 64, ntl = T64r * (T64r + 1) / 2;
+    if (ntl * 128 + (TH / 64) * 512 <= 11328) {
+      double* rowp = smem;                                  // [ntl][64]
+      double* colp = rowp + ntl * 64;                       // [ntl][64]
+      double* rbuf = colp + ntl * 64 + wave * 512;          // [8][64] per wave
+      for (int st = wave; st < ntl; st += TH / 64) {
+        int tI = 0;
+        while ((tI + 1) * (tI + 2) / 2 <= st) ++tI;
+        const int tJ = st - tI * (tI + 1) / 2;
+        const int j = 64 * tJ + lane;  // < np: the nodes past N read as zeros, masked below
+        const bool jv = j < N;
+        const double xj = (double)xs[j], yj = (double)ys[j];
+        double cacc = 0.0;
+        const int rows_t = min(64, N - 64 * tI);
+        for (int m0 = 0; m0 < rows_t; m0 += 8) {
+          double v[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int i = 64 * tI + m0 + q;
+            const bool iv = i < N;
+            const double d = dist64((double)xs[i], (double)ys[i], xj, yj);
+            const double dd = iv && jv ? d : 0.0;
+            v[q] = dd;
+            if (tI > tJ) cacc += dd;
+            dup = dup || (iv && jv && j != i && d == 0.0);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) rbuf[q * 64 + lane] = v[q];
+          wave_sync();
+          const int q = lane & 7, sg = lane >> 3;  // row q of the chunk, columns 8·sg .. 8·sg + 7
+          double rsum = 0.0;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) rsum += rbuf[q * 64 + 8 * sg + c];
+          rsum += __shfl_xor(rsum, 8, 64);
+          rsum += __shfl_xor(rsum, 16, 64);
+          rsum += __shfl_xor(rsum, 32, 64);
+          if (lane < 8) rowp[st * 64 + m0 + q] = rsum;
+          wave_sync();
+        }
+        if (tI > tJ) colp[st * 64 + lane] = cacc;
+      }
+      __syncthreads();
+      for (int i = t; i < N; i += TH) {  // row i: its row block's row partials, then the column partials below
+        const int tI = i >> 6, r = i & 63;
+        double rs = 0.0;
+        for (int tJ = 0; tJ <= tI; ++tJ) rs += rowp[(tI * (tI + 1) / 2 + tJ) * 64 + r];
+        for (int I2 = tI + 1; I2 < T64r; ++I2) rs += colp[(I2 * (I2 + 1) / 2 + tI) * 64 + r];
+        gl[i] = fma(e, rs, -(i < n ? dist(n, i) : 0.0));
+      }
+    } else {
+      constexpr int RB = 4, WV = TH / 64;
+      for (int i0 = wave; i0 < N; i0 += RB * WV) {
+        double rs[RB], xi[RB], yi[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int i = min(i0 + r * WV, N - 1);
+          xi[r] = (double)xs[i], yi[r] = (double)ys[i], rs[r] = 0.0;
+        }
+        for (int j = lane; j < N; j += 64) {
+          const double xj = (double)xs[j], yj = (double)ys[j];
+#pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const double d = dist64(xi[r], yi[r], xj, yj);
+            rs[r] += d;
+            dup = dup || (i0 + r * WV < N && j != i0 + r * WV && d == 0.0);
+          }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+          for (int r = 0; r < RB; ++r) rs[r] += __shfl_xor(rs[r], off, 64);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int i = i0 + r * WV;
+          if (lane == 0 && i < N) gl[i] = fma(e, rs[r], -(i < n ? dist(n, i) : 0.0));
+        }
+      }
+    }
+    if (dup) s_bad = 1;
+    __syncthreads();
+    CH_MARK(1);
+    double ub = 0.0, ug = 0.0;
+    for (int i = t; i < N; i += TH) ub = fma(u(i), zv[i], ub), ug = fma(u(i), gl[i], ug);
+    const double utb = sum_all(ub), b2 = beta * beta * sum_all(ug);
+    auto hah = [&](int i, int j, double d) { return d - beta * (u(i) * gl[j] + gl[i] * u(j)) + b2 * u(i) * u(j); };
+    for (int i = t; i < N; i += TH) {
+      cvl[i] = zv[i] - beta * u(i) * utb;
+      mvl[i] = hah(n, i, i < n ? dist(n, i) : 0.0);
+    }
+    __syncthreads();
+    CH_MARK(2);
+    // element (i, j) of the padded matrix [S | I_pad; c₁ᵀ; mᵀ] (row i, column j < n64), branch-free: for i, j < n,
+    // −hah(i, j, d) = β·e·(g_i + g_j) − d − b2·e² (u = e on both); the right-hand-side rows are their own row group
+    const double be = beta * e, b2e2 = b2 * e * e;
+    auto s_mat = [&](int i, int j, double xi, double yi, double gi) -> double {
+      const double s = fma(be, gi + gl[j], -dist64(xi, yi, (double)xs[j], (double)ys[j]) - b2e2);
+      return i < n ? (j < n ? s : 0.0) : (i == j ? 1.0 : 0.0);
+    };
+    auto s_rhs = [&](int r, int j) -> double {  // row n64 + r
+      const double v = r == 0 ? cvl[j] : mvl[j];
+      return r < 2 && j < n ? v : 0.0;
+    };
+
+    // ---- the factorization, block column by block column -------------------------------------------
+    for (int J = 0; J < nbc && !s_bad; ++J) {  // s_bad: block-uniform after each sync
+      const int J0 = 64 * J, rgd = J0 / 16;
+      for (int rgp = rgd; rgp < G; rgp += PASS) {  // passes of up to 32 row groups
+        const bool p0 = rgp == rgd;
+        int rgt[RGW];
+        bool vt[RGW];
+#pragma unroll
+        for (int tt = 0; tt < RGW; ++tt) rgt[tt] = rgp + wave + NWV * tt, vt[tt] = rgt[tt] < G;
+        static_assert(NWV >= 4, "the 4 diagonal sub-blocks are the first row groups of waves 0..3");
+        const bool dg = p0 && wave < 4;  // this wave's first row group is diagonal sub-block `wave`
+        dx4 acc[RGW][4];
+#pragma unroll
+        for (int tt = 0; tt < RGW; ++tt)
+#pragma unroll
+          for (int cg = 0; cg < 4; ++cg) acc[tt][cg] = dx4{0.0, 0.0, 0.0, 0.0};
+        // Cᵀ[c][i] = Σ_{q < J0} L[J0 + c][q]·L[i][q], one earlier block column K per LDS chunk
+        constexpr int SQ = 2048 / TH;  // double2 per thread of a 32-KB chunk
+        double stg[2 * SQ];
+        auto load_chunk = [&](int K) {  // rows J0 .. J0 + 63 of block column K: 64 consecutive tiles
+          const double2* src = reinterpret_cast<const double2*>(tile(rgd, 16 * K));
+#pragma unroll
+          for (int q = 0; q < SQ; ++q) {
+            const double2 v = src[t + q * TH];
+            stg[2 * q] = v.x, stg[2 * q + 1] = v.y;
+          }
+        };
+        // the row groups this wave holds in this pass are a prefix tt < ntt (wave-uniform): one branch-free K loop per
+        // count, so the inner loop has no per-row-group conditions (every wave still takes every chunk's barrier)
+        const int ntt = max(0, min(RGW, (G - rgp - wave + NWV - 1) / NWV));
+        auto kloop = [&](auto ntc) {
+          constexpr int NT = decltype(ntc)::value;
+          if (J > 0) load_chunk(0);
+          for (int K = 0; K < J; ++K) {
+            double* Ak = Ab + (K & 1) * 4096;
+#pragma unroll
+            for (int q = 0; q < SQ; ++q)
+              reinterpret_cast<double2*>(Ak)[t + q * TH] = make_double2(stg[2 * q], stg[2 * q + 1]);
+            __syncthreads();
+            if (K + 1 < J) load_chunk(K + 1);  // in flight during this chunk's MFMAs
+            if constexpr (NT > 0) {
+              // B operands from the slot (the diagonal row groups' too: the chunk just staged left them in L2)
+              // through a 4-deep ring: column group jl + 4's loads issue behind jl's MFMAs; the scheduling fences keep
+              // the compiler from hoisting all 16 column groups' loads (which spilled)
+              const double* bp[NT];
+#pragma unroll
+              for (int tt = 0; tt < NT; ++tt) bp[tt] = tile(rgt[tt], 16 * K) + lane;
+              double bq[4][NT];
+#pragma unroll
+              for (int d = 0; d < 4; ++d)
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) bq[d][tt] = bp[tt][d * 64];
+#pragma unroll
+              for (int jl = 0; jl < 16; ++jl) {
+                double a[4];
+#pragma unroll
+                for (int cg = 0; cg < 4; ++cg) a[cg] = Ak[(cg * 16 + jl) * 64 + lane];
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+                  for (int cg = 0; cg < 4; ++cg)
+                    acc[tt][cg] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cg], bq[jl & 3][tt], acc[tt][cg], 0, 0, 0);
+                if (jl + 4 < 16)
+#pragma unroll
+                  for (int tt = 0; tt < NT; ++tt) bq[jl & 3][tt] = bp[tt][(jl + 4) * 64];
+                __builtin_amdgcn_sched_barrier(0);
+              }
+            }
+          }
+        };
+        switch (ntt) {
+          case 8: kloop(std::integral_constant<int, 8>{}); break;
+          case 7: kloop(std::integral_constant<int, 7>{}); break;
+          case 6: kloop(std::integral_constant<int, 6>{}); break;
+          case 5: kloop(std::integral_constant<int, 5>{}); break;
+          case 4: kloop(std::integral_constant<int, 4>{}); break;
+          case 3: kloop(std::integral_constant<int, 3>{}); break;
+          case 2: kloop(std::integral_constant<int, 2>{}); break;
+          case 1: kloop(std::integral_constant<int, 1>{}); break;
+          default: kloop(std::integral_constant<int, 0>{}); break;
+        }
+        CH_MARK(3);
+        // C = S − Cᵀ (S from the distances, in registers)
+#pragma unroll
+        for (int tt = 0; tt < RGW; ++tt) {
+          if (!vt[tt]) continue;
+          const int i = 16 * rgt[tt] + lr, ic = i < np ? i : 0;
+          const double xi = (double)xs[ic], yi = (double)ys[ic], gi = gl[ic];
+          const bool rhs = rgt[tt] == G - 1;  // wave-uniform
+#pragma unroll
+          for (int cg = 0; cg < 4; ++cg) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int j = J0 + 16 * cg + 4 * g + lk;
+              acc[tt][cg][g] = (rhs ? s_rhs(lr, j) : s_mat(i, j, xi, yi, gi)) - acc[tt][cg][g];
+            }
+            __builtin_amdgcn_sched_barrier(0);  // (else every distance's operands are hoisted: spills)
+          }
+        }
+        CH_MARK(4);
+        // the four 16-column sub-panels
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // (1) update by the finished sub-panels k < j: acc[j] −= L_D(j, k) · X_k  (rows of the diagonal
+          // sub-block `wave` need sub-panels j <= wave only)
+#pragma unroll
+          for (int tt = 0; tt < RGW; ++tt) {
+            if (!vt[tt] || (tt == 0 && dg && j > wave) || j == 0) continue;
+            dx4 s = dx4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < j; ++k)
+#pragma unroll
+              for (int sl = 0; sl < 4; ++sl)
+                s = __builtin_amdgcn_mfma_f64_16x16x4f64(Dg[(ll_ls(j, k) * 4 + sl) * 64 + lane], acc[tt][k][sl], s, 0, 0, 0);
+            acc[tt][j] -= s;
+          }
+          // (2) the diagonal 16×16 block T: factored AND inverted by wave j in registers, four lanes per row: lane
+          // 4i + g holds T[i][4g .. 4g + 3] and the same columns of W (= I at the start).  Step c: pivot d = T[c][c] by
+          // readlane, s = d^-1/2; T[i][c] reaches the row's quad by a DPP broadcast, column c at the lane's own four
+          // columns (T[k][c], k = 4g + q) and row c of W by ds_bpermute; T[i][k] −= T[i][c]·T[k][c]·s² (c < k <= i),
+          // W[i][k] −= T[i][c]·s · W[c][k]·s (k <= c).  W's rows scaled by their s at the end give L⁻¹ (r05's lane-
+          // per-row form needed 64 VGPRs for the block and its inverse, which spilled the whole kernel; the r06 LDS
+          // form took ≈ 10 µs per leaf)
+          if (p0 && wave == j) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) lf[lr * 17 + 4 * g + lk] = acc[0][j][g];  // lf[i][c] = T[c][i] (symmetric)
+            wave_sync();
+            const int qi = lane >> 2, qg = lane & 3;  // row, column group
+            double ta[4], tw[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ta[q] = lf[qi * 17 + 4 * qg + q], tw[q] = qi == 4 * qg + q ? 1.0 : 0.0;
+            double si = 0.0;
+            bool bad = false;
+            auto bperm = [](int src_lane, double v) {
+              const uint64_t x = __double_as_longlong(v);
+              const uint32_t lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)x);
+              const uint32_t hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(x >> 32));
+              return __longlong_as_double(((uint64_t)hi << 32) | lo);
+            };
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+              const int cq = c & 3, cg = c >> 2;
+              const double d = readlane64(ta[cq], 4 * c + cg);
+              bad = bad || !(d > 0.0);
+              double inv = __builtin_amdgcn_rsq(d);
+              inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
+              inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
+              const double lic = bperm(4 * qi + cg, ta[cq]) * inv;  // L[i][c] (rows i > c are used)
+              if (qi == c) si = inv;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int k = 4 * qg + q;
+                const double lkc = bperm(4 * k + cg, ta[cq]) * inv;  // L[k][c]
+                const double wck = bperm(4 * c + qg, tw[q]) * inv;   // W[c][k]·s
+                if (qi > c && k > c && k <= qi) ta[q] = fma(-lic, lkc, ta[q]);
+                if (qi > c && k <= c) tw[q] = fma(-lic, wck, tw[q]);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+            }
+            // L⁻¹[i][k] = W[i][k]·s_i as the A operand of the sub-panel solves: slab k/4 (= the column group), lane
+            // i + 16·(k % 4)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int k = 4 * qg + q;
+              Dg[(6 + j) * 256 + qg * 64 + qi + 16 * q] = k <= qi ? tw[q] * si : 0.0;
+            }
+            if (bad && lane == 0) s_bad = 1;
+          }
+          __syncthreads();
+          CH_MARK(5);
+          // (3) rows below the diagonal block: X_j = L_jj⁻¹ · acc[j]; the diagonal sub-blocks below publish theirs
+          // as the L_D(wave, j) operand of the later sub-panels
+#pragma unroll
+          for (int tt = 0; tt < RGW; ++tt) {
+            if (!vt[tt] || (tt == 0 && dg && j >= wave)) continue;
+            dx4 s = dx4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int sl = 0; sl < 4; ++sl)
+              s = __builtin_amdgcn_mfma_f64_16x16x4f64(Dg[((6 + j) * 4 + sl) * 64 + lane], acc[tt][j][sl], s, 0, 0, 0);
+            acc[tt][j] = s;
+            if (tt == 0 && dg)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) Dg[(ll_ls(wave, j) * 4 + g) * 64 + lane] = s[g];
+          }
+          __syncthreads();
+          CH_MARK(6);
+        }
+        // L's tiles of this block column (the diagonal sub-blocks go to the slot's diagonal area below)
+#pragma unroll
+        for (int tt = 0; tt < RGW; ++tt) {
+          if (!vt[tt] || rgt[tt] < rgd + 4) continue;
+          double* tb = tile(rgt[tt], 16 * J) + lane;  // the block column's 16 tiles of this row group are consecutive
+#pragma unroll
+          for (int cg = 0; cg < 4; ++cg)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) tb[(4 * cg + g) * 64] = acc[tt][cg][g];
+        }
+        CH_MARK(7);
+        if (s_bad) break;
+      }
+      for (int idx = t; idx < LL_DIAG; idx += TH) diagw[(int64_t)J * LL_DIAG + idx] = Dg[idx];
+      __syncthreads();  // Dg and the A chunks are reused by the next block column
+      CH_MARK(8);
+    }
+
+    if (s_bad) {
+      if (t == 0) atomicExch(status, (int)RTI_ERR_SINGULAR);
+      for (int j = t; j < N; j += TH) wT[(int64_t)j * P + p] = __builtin_nan("");
+      __syncthreads();
+      continue;
+    }
+    // ---- Lᵀ z = y: y = the right-hand-side rows of L (row group G − 1, lanes 0 and 1 of each tile) ------------
+    for (int idx = t; idx < n64; idx += TH) {
+      const double* tl = tile(G - 1, idx >> 2);
+      zv[idx] = tl[16 * (idx & 3)], zv[n64 + idx] = tl[1 + 16 * (idx & 3)];
+    }
+    __syncthreads();
+    for (int J = nbc - 1; J >= 0; --J) {
+      const int J0 = 64 * J, rgd = J0 / 16;
+      // rhs[c] = y[J0 + c] − Σ_{i >= J0 + 64} L[i][J0 + c] z[i]: wave w takes column groups CW·w .. CW·w + CW − 1 of
+      // the block; the row groups' tiles of a column group are 1 KiB apart, RU row groups' loads in flight at a time
+      constexpr int CW = 16 / NWV, RU = 4;
+      double s1[CW], s2[CW];
+#pragma unroll
+      for (int h = 0; h < CW; ++h) s1[h] = 0.0, s2[h] = 0.0;
+      const int rgb = rgd + 4, nrg = G - 1 - rgb;
+      const double* gb = tile(rgb, 16 * J + CW * wave) + lane;  // + (rg − rgb)·1024 + h·64
+      for (int r0 = 0; r0 < nrg; r0 += RU) {
+        double lv[RU][CW], z1[RU], z2[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int rr = min(r0 + u, nrg - 1);
+#pragma unroll
+          for (int h = 0; h < CW; ++h) lv[u][h] = gb[(int64_t)rr * 1024 + h * 64];
+          const bool ok = r0 + u < nrg;
+          z1[u] = ok ? zv[16 * (rgb + rr) + lr] : 0.0, z2[u] = ok ? zv[n64 + 16 * (rgb + rr) + lr] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u)
+#pragma unroll
+          for (int h = 0; h < CW; ++h) s1[h] = fma(lv[u][h], z1[u], s1[h]), s2[h] = fma(lv[u][h], z2[u], s2[h]);
+      }
+#pragma unroll
+      for (int h = 0; h < CW; ++h)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) s1[h] += __shfl_xor(s1[h], off, 64), s2[h] += __shfl_xor(s2[h], off, 64);
+      if (lr == 0) {
+#pragma unroll
+        for (int h = 0; h < CW; ++h) {
+          const int c = 4 * (CW * wave + h) + lk;
+          lf[c] = zv[J0 + c] - s1[h], lf[64 + c] = zv[n64 + J0 + c] - s2[h];
+        }
+      }
+      for (int idx = t; idx < LL_DIAG; idx += TH) Dg[idx] = diagw[(int64_t)J * LL_DIAG + idx];
+      __syncthreads();
+      CH_MARK(9);
+      if (wave == 0) {  // L_Dᵀ z = rhs by 16×16 blocks: lanes 0–15 the first right-hand side, 16–31 the second
+        const int c = lr, rh = lk & 1;
+        double* zl = zv + rh * n64 + J0;
+        // (loops kept rolled: unrolled, the compiler hoisted all 96 LDS operands and spilled the whole kernel)
+#pragma unroll 1
+        for (int j = 3; j >= 0; --j) {
+          double v = lf[rh * 64 + 16 * j + c];
+#pragma unroll 1
+          for (int jp = j + 1; jp < 4; ++jp) {
+            double v2 = 0.0;
+#pragma unroll
+            for (int m = 0; m < 16; m += 2) {
+              v = fma(-Dg[ll_ls(jp, j) * 256 + (c >> 2) * 64 + m + 16 * (c & 3)], zl[16 * jp + m], v);
+              v2 = fma(-Dg[ll_ls(jp, j) * 256 + (c >> 2) * 64 + m + 1 + 16 * (c & 3)], zl[16 * jp + m + 1], v2);
+            }
+            v += v2;
+          }
+          double* tmp = lf + 128 + rh * 16;
+          if (lane < 32) tmp[c] = v;
+          wave_sync();
+          double z = 0.0, z2 = 0.0;
+#pragma unroll
+          for (int cc = 0; cc < 16; cc += 2) {
+            z = fma(Dg[(6 + j) * 256 + (c >> 2) * 64 + cc + 16 * (c & 3)], tmp[cc], z);
+            z2 = fma(Dg[(6 + j) * 256 + (c >> 2) * 64 + cc + 1 + 16 * (c & 3)], tmp[cc + 1], z2);
+          }
+          z += z2;
+          if (lane < 32) zl[16 * j + c] = z;
+          wave_sync();
+        }
+      }
+      __syncthreads();
+      CH_MARK(10);
+    }
+    // bordered elimination: y_n = (c_n + mᵀz1)/(μ + mᵀz2), y₁ = −z1 + z2·y_n, w = H y
+    double a1 = 0.0, a2 = 0.0;
+    for (int i = t; i < n; i += TH) a1 = fma(mvl[i], zv[i], a1), a2 = fma(mvl[i], zv[n64 + i], a2);
+    const double mz1 = sum_all(a1), mz2 = sum_all(a2);
+    const double yn = (cvl[n] + mz1) / (mvl[n] + mz2);
+    double uy = 0.0;
+    for (int i = t; i < N; i += TH) uy = fma(u(i), i < n ? -zv[i] + zv[n64 + i] * yn : yn, uy);
+    const double uty = sum_all(uy);
+    for (int i = t; i < N; i += TH) {
+      const double yi = i < n ? -zv[i] + zv[n64 + i] * yn : yn;
+      wT[(int64_t)i * P + p] = yi - beta * u(i) * uty;
+    }
+    __syncthreads();  // the slot and the LDS are reused by the next pixel
+    CH_MARK(11);
+  }
+#ifdef RTI_CHOL_PROFILE
+  if (t == 0 && blockIdx.x < 1024)
+    for (int k = 0; k < 16; ++k) rti_chol_prof[blockIdx.x][k] = prof_[k];
+#endif
+}
+
 // fp64 register Gauss-Jordan up to here, rbf_solve_gji above (solve of a 400×400 ROI, MI355X:
 // N = 64: 6.3 vs 13.2 ms, N = 96: 27.9 vs 18.1 ms; tools/time_rbf_solve.py)
 constexpr int RBF_GJ_MAX_N = 80;
@@ -1515,6 +2048,13 @@ int gji_refine() {
 }
 
 bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); }
+// (r06) the left-looking matrix-core Cholesky for 256 < N <= RBF_LL_MAX_N; RTI_RBF_CHOL_OLD=1 (environment, read per
+// call: a measurement switch) keeps the right-looking rbf_solve_chol for A/B
+bool uses_llt(int N) {
+  if (N <= RBF_MAX_N || N > RBF_LL_MAX_N) return false;
+  const char* e = getenv("RTI_RBF_CHOL_OLD");
+  return !(e && atoi(e));
+}
 
 // redo / fb_ws: the fallback's pixel list (redo[0] = count, zeroed) and its workspace, when uses_gji(N)
 template <typename T>
@@ -1525,6 +2065,13 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
   const dim3 g((unsigned)P);
   if (N > RBF_MAX_N) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
     const unsigned cg = (unsigned)(P < chol_grid ? P : chol_grid);
+    if (uses_llt(N)) {  // (r06) left-looking on the matrix cores
+      const size_t lds = ll_lds_bytes(N);
+      (void)reserve_lds(reinterpret_cast<const void*>(rbf_solve_llt<T>), lds);
+      hipLaunchKernelGGL((rbf_solve_llt<T>), dim3(cg), dim3(RBF_LL_TH), lds, s, lu, lv, In, N, P, wT, xyT, status,
+                         fb_ws);
+      return;
+    }
     auto go = [&](auto kern, int nb) {
       const size_t lds = chol_lds_bytes(N, nb);
       (void)reserve_lds(reinterpret_cast<const void*>(kern), lds);
@@ -1637,7 +2184,8 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
   int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
-  const int64_t slot_doubles = N > RBF_CH_MAX_N ? chol_slot_doubles_gp(N) : chol_slot_doubles(N);
+  const int64_t slot_doubles = N > RBF_CH_MAX_N ? chol_slot_doubles_gp(N) : uses_llt(N) ? ll_slot_doubles(N)
+                                                                                 : chol_slot_doubles(N);
   const size_t node_bytes = (size_t)N * P * (sizeof(double) + sizeof(float2));
   if (chol && N > RBF_CH_MAX_N) {  // GP slots (≈ 4·N² bytes each): as many workgroups as the budget holds
     const int64_t fit = (int64_t)(gp_ws_budget(node_bytes) / ((size_t)slot_doubles * sizeof(double)));

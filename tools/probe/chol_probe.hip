@@ -57,9 +57,14 @@ int main(int argc, char** argv) {
   (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const int G = (int)(P < cus ? P : cus);
-  const char* names[14] = {"load", "A+rowsum", "g colsum", "c,m,S", "stage", "diag factor", "trsm+fwd diag",
-                           "writeback+fwd upd", "trailing", "backward (rest)", "final", "  bwd: loads+stage",
-                           "  bwd: diag solve", "  bwd: update"};
+  const char* names_rl[14] = {"load", "A+rowsum", "g colsum", "c,m,S", "stage", "diag factor", "trsm+fwd diag",
+                              "writeback+fwd upd", "trailing", "backward (rest)", "final", "  bwd: loads+stage",
+                              "  bwd: diag solve", "  bwd: update"};
+  // (r06) the left-looking matrix-core form (rbf_solve_llt) marks its own phases
+  const char* names_ll[14] = {"load", "rowsum", "c,m", "update (K chunks)", "S init", "sub-panel upd + leaf",
+                              "sub-panel solve", "L tile stores", "diag area copy", "bwd: GEMV", "bwd: diag solve",
+                              "final", "-", "-"};
+  const char** names = uses_llt(N) ? names_ll : names_rl;
   double tot = 0;
   for (int k = 0; k < 14; ++k) {
     double s = 0;
