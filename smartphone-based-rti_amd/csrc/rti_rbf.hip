@@ -37,6 +37,27 @@ __device__ __forceinline__ double dist64(double xi, double yi, double xj, double
   return sqrt(dx * dx + dy * dy);
 }
 
+// The correctly rounded fp64 sqrt for 0 <= s < 2^767 (squared distances of nodes in [-1, 1]²: never denormal): LLVM's
+// own expansion of sqrt() (v_rsq_f64 seed, two Newton-Goldschmidt steps, the final residual correction) without its
+// scaling for s < 2^-767 and its inf/NaN fixup, s = 0 selected directly — the same bits in 13 instead of 18 VALU ops.
+// (r06: the left-looking Cholesky evaluates ≈ 1.5·N² distances per pixel.)
+__device__ __forceinline__ double sqrt_pos(double s) {
+  const double y = __builtin_amdgcn_rsq(s);
+  double g = s * y, h = 0.5 * y;
+  const double r = fma(-g, h, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, s);
+  g = fma(d, h, g);
+  d = fma(-g, g, s);
+  g = fma(d, h, g);
+  return s == 0.0 ? 0.0 : g;
+}
+__device__ __forceinline__ double dist64_pos(double xi, double yi, double xj, double yj) {
+  const double dx = xi - xj, dy = yi - yj;
+  return sqrt_pos(dx * dx + dy * dy);
+}
+
 // ‖·‖ for the evaluation sweep: the fp64 rsq approximation and one Newton step,
 // d = s·r + (s − (s·r)²)·r/2 — 8 issue slots against ≈ 17 for the correctly rounded fp64 sqrt.
 // (The fp32 rsq seed with conversions and a clamp ran at the same speed on MI355X, 229.6 vs 230.4 ms
@@ -1519,10 +1540,14 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
 // Slot traffic per pixel at N = 400: ≈ 2.0 MB of B/A tiles read, 0.9 MB of L written, 0.9 MB read back by the
 // backward pass — against ≈ 8 MB for the right-looking panels (each panel re-read and re-wrote the trailing
 // triangle).  A non-positive pivot (repeated or nearly repeated nodes) reports RTI_ERR_SINGULAR like rbf_solve_chol.
-// 8 waves (two per SIMD, 256 registers each) of 4 row groups.  (4 waves of 8 row groups, 512 registers each with the
-// accumulators in AGPRs, spilled far more: 738 VGPRs)
-constexpr int RBF_LL_TH = 512;
+// TWO pixels per CU: workgroups of 4 waves (one per SIMD) with 256 registers each (amdgpu_waves_per_eu(2)) and at
+// most half the LDS, so one pixel's serial phases (the 16×16 leaves, the barriers, the distance evaluations on the
+// VALU) run while the other pixel's waves keep the matrix cores busy.  (One 8-wave workgroup per CU: 333.7 ms at
+// N = 400; 4 waves of 8 row groups with 512 registers each spilled 738 VGPRs.)
+// Above N = 448 the LDS no longer fits twice per CU: one workgroup of 8 waves per CU instead (RBF_LL_TH1).
+constexpr int RBF_LL_TH = 256, RBF_LL_TH1 = 512;
 constexpr int RBF_LL_RGW = 4;  // row groups per wave per pass (16 accumulator tiles)
+constexpr int RBF_LL_TWO_MAX_N = 448;
 constexpr int RBF_LL_MAX_N = 1022;
 __host__ __device__ constexpr int ll_n64(int N) { return (N - 1 + 63) / 64 * 64; }
 __host__ __device__ constexpr int ll_groups(int N) { return ll_n64(N) / 16 + 1; }  // + the right-hand-side group
@@ -1532,19 +1557,22 @@ constexpr int LL_DIAG = 2560;  // per block column: 6 off-diagonal 16×16 blocks
 __host__ __device__ constexpr int64_t ll_slot_doubles(int N) {
   return ll_col_tiles(ll_groups(N), ll_n64(N) / 64) * 1024 + (int64_t)(ll_n64(N) / 64) * LL_DIAG;
 }
-// LDS: A chunks [2][4096], the block column's L_D blocks / inverses [2560], the leaf's two 16×17 matrices and pivots
-// (backward: 2×64 right-hand sides) [576], z [2][n64], g, c, m [np] each, the nodes [2][np] floats; np = n64 + 64 >= N, the entries past N
-// zero, so every column index j < n64 reads in bounds and the (many) per-column loads share one base address
+// LDS: the A chunk [4096], the block column's L_D blocks / inverses [2560], the leaf's 16×17 matrix (backward: 2×64
+// right-hand sides) [576], z [2][n64], g, c, m [np] each, the nodes [2][np] floats; np = n64 + 64 >= N, the entries
+// past N zero, so every column index j < n64 reads in bounds and the (many) per-column loads share one base address.
+// Up to N = 448 that is <= 80 KiB: two workgroups per CU.
+constexpr int LL_OFF_DG = 4096, LL_OFF_LF = LL_OFF_DG + 2560, LL_OFF_Z = LL_OFF_LF + 576;
 __host__ __device__ constexpr int ll_np(int N) { return ll_n64(N) + 64; }
-__host__ __device__ constexpr size_t ll_lds_bytes(int N) { return (size_t)(11328 + 2 * ll_n64(N) + 4 * ll_np(N)) * 8; }
+__host__ __device__ constexpr size_t ll_lds_bytes(int N) { return (size_t)(LL_OFF_Z + 2 * ll_n64(N) + 4 * ll_np(N)) * 8; }
+static_assert(ll_lds_bytes(448) + 64 <= 80 * 1024, "two workgroups per CU at N <= 448");
 static_assert(ll_lds_bytes(RBF_LL_MAX_N) <= 160 * 1024 - 256, "RBF_LL_MAX_N");
 __host__ __device__ constexpr int ll_ls(int jp, int j) { return jp * (jp - 1) / 2 + j; }  // L_D block (jp, j), jp > j
 
-template <typename T>
-__global__ void __launch_bounds__(RBF_LL_TH)
+template <typename T, int TH>
+__global__ void __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(2, 2)))
 rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
               double* __restrict__ wT, float2* __restrict__ xyT, int* __restrict__ status, double* __restrict__ ws) {
-  constexpr int TH = RBF_LL_TH, RGW = RBF_LL_RGW, NWV = TH / 64, PASS = NWV * RGW;  // PASS = 32 row groups
+  constexpr int RGW = RBF_LL_RGW, NWV = TH / 64, PASS = NWV * RGW;  // row groups per pass
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // wave index through readfirstlane: the compiler then knows every wave-dependent condition (row groups, diagonal
   // sub-blocks) is uniform and branches on SCC instead of masking EXEC around the MFMAs
@@ -1553,10 +1581,10 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
   const int n = N - 1, n64 = ll_n64(N), nbc = n64 / 64, G = n64 / 16 + 1;
   double* slot = ws + (int64_t)blockIdx.x * ll_slot_doubles(N);
   double* diagw = slot + ll_col_tiles(G, nbc) * 1024;  // [nbc][LL_DIAG]
-  double* Ab = smem;                                   // [2][4096]: A chunks, tiles [c-group][jl][64]
-  double* Dg = smem + 8192;                            // [10][4][64]: L_D(jp, j) (6), then the inverses (4)
-  double* lf = smem + 10752;                           // [576] the leaf; backward: [2][64] right-hand sides + [2][16]
-  double* zv = smem + 11328;                           // [2][n64]
+  double* Ab = smem;                                   // [4096]: the A chunk, tiles [c-group][jl][64]
+  double* Dg = smem + LL_OFF_DG;                       // [10][4][64]: L_D(jp, j) (6), then the inverses (4)
+  double* lf = smem + LL_OFF_LF;                       // [576] the leaf; backward: [2][64] right-hand sides + [2][16]
+  double* zv = smem + LL_OFF_Z;                        // [2][n64]
   const int np = ll_np(N);
   double* gl = zv + 2 * n64;                           // g = A u
   double* cvl = gl + np;                               // c = H b
@@ -1614,7 +1642,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
     // row's sum added up in a fixed order; otherwise RB rows per wave, every distance of a row
     bool dup = false;
     const int T64r = (N + 63) / 64, ntl = T64r * (T64r + 1) / 2;
-    if (ntl * 128 + (TH / 64) * 512 <= 11328) {
+    if (ntl * 128 + (TH / 64) * 512 <= LL_OFF_Z) {
       double* rowp = smem;                                  // [ntl][64]
       double* colp = rowp + ntl * 64;                       // [ntl][64]
       double* rbuf = colp + ntl * 64 + wave * 512;          // [8][64] per wave
@@ -1633,7 +1661,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           for (int q = 0; q < 8; ++q) {
             const int i = 64 * tI + m0 + q;
             const bool iv = i < N;
-            const double d = dist64((double)xs[i], (double)ys[i], xj, yj);
+            const double d = dist64_pos((double)xs[i], (double)ys[i], xj, yj);
             const double dd = iv && jv ? d : 0.0;
             v[q] = dd;
             if (tI > tJ) cacc += dd;
@@ -1675,7 +1703,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           const double xj = (double)xs[j], yj = (double)ys[j];
 #pragma unroll
           for (int r = 0; r < RB; ++r) {
-            const double d = dist64(xi[r], yi[r], xj, yj);
+            const double d = dist64_pos(xi[r], yi[r], xj, yj);
             rs[r] += d;
             dup = dup || (i0 + r * WV < N && j != i0 + r * WV && d == 0.0);
           }
@@ -1707,15 +1735,15 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
     // element (i, j) of the padded matrix [S | I_pad; c₁ᵀ; mᵀ] (row i, column j < n64), branch-free: for i, j < n,
     // −hah(i, j, d) = β·e·(g_i + g_j) − d − b2·e² (u = e on both); the right-hand-side rows are their own row group
     const double be = beta * e, b2e2 = b2 * e * e;
-    auto s_mat = [&](int i, int j, double xi, double yi, double gi) -> double {
-      const double s = fma(be, gi + gl[j], -dist64(xi, yi, (double)xs[j], (double)ys[j]) - b2e2);
-      return i < n ? (j < n ? s : 0.0) : (i == j ? 1.0 : 0.0);
+    // (the column index enters as j = J0 + lk + o with o = 16·cg + 4·g a compile-time offset: the per-element tests
+    // are one compare against that immediate and one against a scalar, and the loads share one base — r06: with j
+    // itself per element the compiler kept 16 column indices per lane, spilled them, and waited on a scratch reload
+    // for every element)
+    auto s_mat = [&](bool iv, int di, int jrem, int o, const float* xj, const float* yj, const double* gj, double xi,
+                     double yi, double gi) -> double {  // di = i − J0 − lk; jrem = n − J0 − lk (j < n ⟺ o < jrem)
+      const double s = fma(be, gi + gj[o], -dist64_pos(xi, yi, (double)xj[o], (double)yj[o]) - b2e2);
+      return iv ? (o < jrem ? s : 0.0) : (di == o ? 1.0 : 0.0);
     };
-    auto s_rhs = [&](int r, int j) -> double {  // row n64 + r
-      const double v = r == 0 ? cvl[j] : mvl[j];
-      return r < 2 && j < n ? v : 0.0;
-    };
-
     // ---- the factorization, block column by block column -------------------------------------------
     for (int J = 0; J < nbc && !s_bad; ++J) {  // s_bad: block-uniform after each sync
       const int J0 = 64 * J, rgd = J0 / 16;
@@ -1733,14 +1761,17 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
 #pragma unroll
           for (int cg = 0; cg < 4; ++cg) acc[tt][cg] = dx4{0.0, 0.0, 0.0, 0.0};
         // Cᵀ[c][i] = Σ_{q < J0} L[J0 + c][q]·L[i][q], one earlier block column K per LDS chunk
-        constexpr int SQ = 2048 / TH;  // double2 per thread of a 32-KB chunk
-        double stg[2 * SQ];
-        auto load_chunk = [&](int K) {  // rows J0 .. J0 + 63 of block column K: 64 consecutive tiles
+        // one earlier block column K per chunk: rows J0 .. J0 + 63 of K (64 consecutive tiles, 32 KB) staged in LDS
+        auto stage_chunk = [&](int K) {
+          constexpr int SQ = 2048 / TH;  // double2 per thread
           const double2* src = reinterpret_cast<const double2*>(tile(rgd, 16 * K));
 #pragma unroll
-          for (int q = 0; q < SQ; ++q) {
-            const double2 v = src[t + q * TH];
-            stg[2 * q] = v.x, stg[2 * q + 1] = v.y;
+          for (int h = 0; h < SQ; h += 4) {
+            double2 v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = src[t + (h + q) * TH];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) reinterpret_cast<double2*>(Ab)[t + (h + q) * TH] = v[q];
           }
         };
         // the row groups this wave holds in this pass are a prefix tt < ntt (wave-uniform): one branch-free K loop per
@@ -1748,26 +1779,28 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
         const int ntt = max(0, min(RGW, (G - rgp - wave + NWV - 1) / NWV));
         auto kloop = [&](auto ntc) {
           constexpr int NT = decltype(ntc)::value;
-          if (J > 0) load_chunk(0);
-          for (int K = 0; K < J; ++K) {
-            double* Ak = Ab + (K & 1) * 4096;
-#pragma unroll
-            for (int q = 0; q < SQ; ++q)
-              reinterpret_cast<double2*>(Ak)[t + q * TH] = make_double2(stg[2 * q], stg[2 * q + 1]);
-            __syncthreads();
-            if (K + 1 < J) load_chunk(K + 1);  // in flight during this chunk's MFMAs
-            if constexpr (NT > 0) {
-              // B operands from the slot (the diagonal row groups' too: the chunk just staged left them in L2)
-              // through a 4-deep ring: column group jl + 4's loads issue behind jl's MFMAs; the scheduling fences keep
-              // the compiler from hoisting all 16 column groups' loads (which spilled)
-              const double* bp[NT];
-#pragma unroll
-              for (int tt = 0; tt < NT; ++tt) bp[tt] = tile(rgt[tt], 16 * K) + lane;
-              double bq[4][NT];
+          // B operands from the slot (the diagonal row groups' too: the chunk just staged left them in L2) through a
+          // 4-deep ring that runs across the chunks: column group jl + 4's loads issue behind jl's MFMAs, the next
+          // chunk's first four during this chunk's last four (the tiles were written block columns ago: no barrier
+          // orders them); the scheduling fences keep the compiler from hoisting all 16 column groups' loads (spills)
+          [[maybe_unused]] double bq[4][NT > 0 ? NT : 1];
+          auto ldb = [&](int K, int jl, int tt) { return tile(rgt[tt], 16 * K + jl)[lane]; };
+          if constexpr (NT > 0) {
+            if (J > 0)
 #pragma unroll
               for (int d = 0; d < 4; ++d)
 #pragma unroll
-                for (int tt = 0; tt < NT; ++tt) bq[d][tt] = bp[tt][d * 64];
+                for (int tt = 0; tt < NT; ++tt) bq[d][tt] = ldb(0, d, tt);
+          }
+          for (int K = 0; K < J; ++K) {
+            const double* Ak = Ab;
+            stage_chunk(K);
+            __syncthreads();
+            if constexpr (NT > 0) {
+              const double* bp[NT];
+#pragma unroll
+              for (int tt = 0; tt < NT; ++tt) bp[tt] = tile(rgt[tt], 16 * K) + lane;
+              const int kn = K + 1 < J ? K + 1 : K;  // (the last chunk re-reads its own first tiles: harmless)
 #pragma unroll
               for (int jl = 0; jl < 16; ++jl) {
                 double a[4];
@@ -1778,19 +1811,16 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
 #pragma unroll
                   for (int cg = 0; cg < 4; ++cg)
                     acc[tt][cg] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cg], bq[jl & 3][tt], acc[tt][cg], 0, 0, 0);
-                if (jl + 4 < 16)
 #pragma unroll
-                  for (int tt = 0; tt < NT; ++tt) bq[jl & 3][tt] = bp[tt][(jl + 4) * 64];
+                for (int tt = 0; tt < NT; ++tt) bq[jl & 3][tt] = jl + 4 < 16 ? bp[tt][(jl + 4) * 64] : ldb(kn, jl - 12, tt);
                 __builtin_amdgcn_sched_barrier(0);
               }
             }
+            __syncthreads();  // the chunk is rewritten by the next K
           }
         };
+        static_assert(RGW == 4, "the K-loop dispatch below");
         switch (ntt) {
-          case 8: kloop(std::integral_constant<int, 8>{}); break;
-          case 7: kloop(std::integral_constant<int, 7>{}); break;
-          case 6: kloop(std::integral_constant<int, 6>{}); break;
-          case 5: kloop(std::integral_constant<int, 5>{}); break;
           case 4: kloop(std::integral_constant<int, 4>{}); break;
           case 3: kloop(std::integral_constant<int, 3>{}); break;
           case 2: kloop(std::integral_constant<int, 2>{}); break;
@@ -1804,13 +1834,22 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           if (!vt[tt]) continue;
           const int i = 16 * rgt[tt] + lr, ic = i < np ? i : 0;
           const double xi = (double)xs[ic], yi = (double)ys[ic], gi = gl[ic];
-          const bool rhs = rgt[tt] == G - 1;  // wave-uniform
+          const bool iv = i < n;
+          const int di = i - J0 - lk, jrem = n - J0 - lk;
+          const float* xj = xs + J0 + lk;
+          const float* yj = ys + J0 + lk;
+          const double* gj = gl + J0 + lk;
+          const double* cj = cvl + J0 + lk;
+          const double* mj = mvl + J0 + lk;
+          const bool rhs = rgt[tt] == G - 1;  // wave-uniform: the right-hand-side rows n64 + lr (c₁ for lr = 0, m for 1)
 #pragma unroll
           for (int cg = 0; cg < 4; ++cg) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              const int j = J0 + 16 * cg + 4 * g + lk;
-              acc[tt][cg][g] = (rhs ? s_rhs(lr, j) : s_mat(i, j, xi, yi, gi)) - acc[tt][cg][g];
+              const int o = 16 * cg + 4 * g;
+              const double v = rhs ? (lr < 2 && o < jrem ? (lr == 0 ? cj[o] : mj[o]) : 0.0)
+                                   : s_mat(iv, di, jrem, o, xj, yj, gj, xi, yi, gi);
+              acc[tt][cg][g] = v - acc[tt][cg][g];
             }
             __builtin_amdgcn_sched_barrier(0);  // (else every distance's operands are hoisted: spills)
           }
@@ -1870,8 +1909,9 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
                 const int k = 4 * qg + q;
                 const double lkc = bperm(4 * k + cg, ta[cq]) * inv;  // L[k][c]
                 const double wck = bperm(4 * c + qg, tw[q]) * inv;   // W[c][k]·s
-                if (qi > c && k > c && k <= qi) ta[q] = fma(-lic, lkc, ta[q]);
-                if (qi > c && k <= c) tw[q] = fma(-lic, wck, tw[q]);
+                const double tu = fma(-lic, lkc, ta[q]), wu = fma(-lic, wck, tw[q]);  // branch-free: selects, no EXEC
+                ta[q] = qi > c && k > c && k <= qi ? tu : ta[q];
+                tw[q] = qi > c && k <= c ? wu : tw[q];
               }
               __builtin_amdgcn_sched_barrier(0);
             }
@@ -1933,16 +1973,19 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
       zv[idx] = tl[16 * (idx & 3)], zv[n64 + idx] = tl[1 + 16 * (idx & 3)];
     }
     __syncthreads();
-    for (int J = nbc - 1; J >= 0; --J) {
-      const int J0 = 64 * J, rgd = J0 / 16;
-      // rhs[c] = y[J0 + c] − Σ_{i >= J0 + 64} L[i][J0 + c] z[i]: wave w takes column groups CW·w .. CW·w + CW − 1 of
-      // the block; the row groups' tiles of a column group are 1 KiB apart, RU row groups' loads in flight at a time
-      constexpr int CW = 16 / NWV, RU = 4;
-      double s1[CW], s2[CW];
+    // Per block column J (last to first): rhs = y_J − Σ_{i >= J0 + 64} L[i][J-block]ᵀ z_i (a GEMV over its tiles, wave w
+    // taking column groups CW·w .. CW·w + CW − 1, RU row groups' loads in flight), then L_Dᵀ z_J = rhs on wave 0.  The
+    // GEMV is software-pipelined across J: the rows beyond block J + 1 have their z before block J + 1's diagonal solve,
+    // so that part of J's GEMV runs DURING it (wave 0 first takes its own share); after the barrier only block J + 1's
+    // four row groups are left.  The partial sums stay in registers across the barrier.
+    constexpr int CW = 16 / NWV, RU = 4;
+    double s1[CW], s2[CW];
 #pragma unroll
-      for (int h = 0; h < CW; ++h) s1[h] = 0.0, s2[h] = 0.0;
-      const int rgb = rgd + 4, nrg = G - 1 - rgb;
-      const double* gb = tile(rgb, 16 * J + CW * wave) + lane;  // + (rg − rgb)·1024 + h·64
+    for (int h = 0; h < CW; ++h) s1[h] = 0.0, s2[h] = 0.0;
+    auto gemv = [&](int J, int rg0, int rg1) {  // rows of row groups [rg0, rg1) of block column J into s1, s2
+      const int nrg = rg1 - rg0;
+      if (nrg <= 0) return;
+      const double* gb = tile(rg0, 16 * J + CW * wave) + lane;  // + (rg − rg0)·1024 + h·64
       for (int r0 = 0; r0 < nrg; r0 += RU) {
         double lv[RU][CW], z1[RU], z2[RU];
 #pragma unroll
@@ -1951,13 +1994,17 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
 #pragma unroll
           for (int h = 0; h < CW; ++h) lv[u][h] = gb[(int64_t)rr * 1024 + h * 64];
           const bool ok = r0 + u < nrg;
-          z1[u] = ok ? zv[16 * (rgb + rr) + lr] : 0.0, z2[u] = ok ? zv[n64 + 16 * (rgb + rr) + lr] : 0.0;
+          z1[u] = ok ? zv[16 * (rg0 + rr) + lr] : 0.0, z2[u] = ok ? zv[n64 + 16 * (rg0 + rr) + lr] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < RU; ++u)
 #pragma unroll
           for (int h = 0; h < CW; ++h) s1[h] = fma(lv[u][h], z1[u], s1[h]), s2[h] = fma(lv[u][h], z2[u], s2[h]);
       }
+    };
+    for (int J = nbc - 1; J >= 0; --J) {
+      const int J0 = 64 * J, rgd = J0 / 16;
+      if (J + 1 < nbc) gemv(J, rgd + 4, rgd + 8);  // block J + 1's rows (its z_{J+1} was solved last iteration)
 #pragma unroll
       for (int h = 0; h < CW; ++h)
 #pragma unroll
@@ -1969,9 +2016,12 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           lf[c] = zv[J0 + c] - s1[h], lf[64 + c] = zv[n64 + J0 + c] - s2[h];
         }
       }
+#pragma unroll
+      for (int h = 0; h < CW; ++h) s1[h] = 0.0, s2[h] = 0.0;
       for (int idx = t; idx < LL_DIAG; idx += TH) Dg[idx] = diagw[(int64_t)J * LL_DIAG + idx];
       __syncthreads();
       CH_MARK(9);
+      if (J > 0) gemv(J - 1, rgd + 4, G - 1);  // block column J − 1's rows beyond block J: their z are final
       if (wave == 0) {  // L_Dᵀ z = rhs by 16×16 blocks: lanes 0–15 the first right-hand side, 16–31 the second
         const int c = lr, rh = lk & 1;
         double* zl = zv + rh * n64 + J0;
@@ -2065,11 +2115,12 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
   const dim3 g((unsigned)P);
   if (N > RBF_MAX_N) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
     const unsigned cg = (unsigned)(P < chol_grid ? P : chol_grid);
-    if (uses_llt(N)) {  // (r06) left-looking on the matrix cores
+    if (uses_llt(N)) {  // (r06) left-looking on the matrix cores: two 4-wave pixels per CU, or one 8-wave
       const size_t lds = ll_lds_bytes(N);
-      (void)reserve_lds(reinterpret_cast<const void*>(rbf_solve_llt<T>), lds);
-      hipLaunchKernelGGL((rbf_solve_llt<T>), dim3(cg), dim3(RBF_LL_TH), lds, s, lu, lv, In, N, P, wT, xyT, status,
-                         fb_ws);
+      auto kern = N <= RBF_LL_TWO_MAX_N ? rbf_solve_llt<T, RBF_LL_TH> : rbf_solve_llt<T, RBF_LL_TH1>;
+      (void)reserve_lds(reinterpret_cast<const void*>(kern), lds);
+      hipLaunchKernelGGL(kern, dim3(cg), dim3(N <= RBF_LL_TWO_MAX_N ? RBF_LL_TH : RBF_LL_TH1), lds, s, lu, lv, In, N, P,
+                         wT, xyT, status, fb_ws);
       return;
     }
     auto go = [&](auto kern, int nb) {
@@ -2183,7 +2234,8 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   // + for the block solvers: the fp64 fallback's pixel list and (N > RBF_FB_LDS_N) per-workgroup matrices
   const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
-  int64_t chol_grid = chol ? (P < device_cus() ? P : device_cus()) : 0;
+  int64_t chol_grid = chol ? (uses_llt(N) && N <= RBF_LL_TWO_MAX_N ? 2 * (int64_t)device_cus() : device_cus()) : 0;
+  if (chol_grid > P) chol_grid = P;
   const int64_t slot_doubles = N > RBF_CH_MAX_N ? chol_slot_doubles_gp(N) : uses_llt(N) ? ll_slot_doubles(N)
                                                                                  : chol_slot_doubles(N);
   const size_t node_bytes = (size_t)N * P * (sizeof(double) + sizeof(float2));

@@ -56,7 +56,8 @@ int main(int argc, char** argv) {
   int rate_khz = 0, cus = 0;
   (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const int G = (int)(P < cus ? P : cus);
+  const int wg = uses_llt(N) && N <= RBF_LL_TWO_MAX_N ? 2 * cus : cus;  // (r06: up to 448 lights two pixels per CU)
+  const int G = (int)(P < wg ? P : wg);
   const char* names_rl[14] = {"load", "A+rowsum", "g colsum", "c,m,S", "stage", "diag factor", "trsm+fwd diag",
                               "writeback+fwd upd", "trailing", "backward (rest)", "final", "  bwd: loads+stage",
                               "  bwd: diag solve", "  bwd: update"};

@@ -33,12 +33,16 @@ def main():
     stream = torch.cuda.current_stream(dev)
     variants = args.gy.split(",")
 
-    def run(v):  # "auto", a grid.y, or "plain" (plain instead of non-temporal table stores)
+    def run(v):  # "auto", a grid.y, "plain" (plain instead of non-temporal table stores) or "xcd" (r06: XCD-
+        # contiguous tile order, RTI_OP_XCD=1)
         os.environ.pop("RTI_OP_PLAIN_STORES", None)
-        if v in ("auto", "plain"):
+        os.environ.pop("RTI_OP_XCD", None)
+        if v in ("auto", "plain", "xcd"):
             os.environ.pop("RTI_OP_GY", None)
             if v == "plain":
                 os.environ["RTI_OP_PLAIN_STORES"] = "1"
+            if v == "xcd":
+                os.environ["RTI_OP_XCD"] = "1"
         else:
             os.environ["RTI_OP_GY"] = v
         wl.step(0)
