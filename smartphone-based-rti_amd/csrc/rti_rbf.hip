@@ -1547,7 +1547,7 @@ rbf_solve_chol(const float* __restrict__ lu, const float* __restrict__ lv, const
 // Above N = 448 the LDS no longer fits twice per CU: one workgroup of 8 waves per CU instead (RBF_LL_TH1).
 constexpr int RBF_LL_TH = 256, RBF_LL_TH1 = 512;
 constexpr int RBF_LL_RGW = 4;  // row groups per wave per pass (16 accumulator tiles)
-constexpr int RBF_LL_TWO_MAX_N = 448;
+constexpr int RBF_LL_TWO_MAX_N = 641;
 constexpr int RBF_LL_MAX_N = 1022;
 __host__ __device__ constexpr int ll_n64(int N) { return (N - 1 + 63) / 64 * 64; }
 __host__ __device__ constexpr int ll_groups(int N) { return ll_n64(N) / 16 + 1; }  // + the right-hand-side group
@@ -1557,14 +1557,15 @@ constexpr int LL_DIAG = 2560;  // per block column: 6 off-diagonal 16×16 blocks
 __host__ __device__ constexpr int64_t ll_slot_doubles(int N) {
   return ll_col_tiles(ll_groups(N), ll_n64(N) / 64) * 1024 + (int64_t)(ll_n64(N) / 64) * LL_DIAG;
 }
-// LDS: the A chunk [4096], the block column's L_D blocks / inverses [2560], the leaf's 16×17 matrix (backward: 2×64
-// right-hand sides) [576], z [2][n64], g, c, m [np] each, the nodes [2][np] floats; np = n64 + 64 >= N, the entries
-// past N zero, so every column index j < n64 reads in bounds and the (many) per-column loads share one base address.
-// Up to N = 448 that is <= 80 KiB: two workgroups per CU.
-constexpr int LL_OFF_DG = 4096, LL_OFF_LF = LL_OFF_DG + 2560, LL_OFF_Z = LL_OFF_LF + 576;
+// LDS: the A chunk [4096] (the backward pass's z [2][n64] in its place), the block column's L_D blocks / inverses
+// [2560], the leaf's 16×17 matrix (backward: 2×64 right-hand sides) [576], g, c, m [np] each, the nodes [2][np]
+// floats; np = n64 + 64 >= N, the entries past N zero, so every column index j < n64 reads in bounds and the (many)
+// per-column loads share one base address.  Up to N = 641 that is <= 80 KiB: two workgroups per CU.
+constexpr int LL_OFF_DG = 4096, LL_OFF_LF = LL_OFF_DG + 2560, LL_OFF_G = LL_OFF_LF + 576;
 __host__ __device__ constexpr int ll_np(int N) { return ll_n64(N) + 64; }
-__host__ __device__ constexpr size_t ll_lds_bytes(int N) { return (size_t)(LL_OFF_Z + 2 * ll_n64(N) + 4 * ll_np(N)) * 8; }
-static_assert(ll_lds_bytes(448) + 64 <= 80 * 1024, "two workgroups per CU at N <= 448");
+__host__ __device__ constexpr size_t ll_lds_bytes(int N) { return (size_t)(LL_OFF_G + 4 * ll_np(N)) * 8; }
+static_assert(ll_lds_bytes(RBF_LL_TWO_MAX_N) + 64 <= 80 * 1024 && 2 * ll_n64(RBF_LL_MAX_N) <= LL_OFF_DG,
+              "two workgroups per CU; z fits in the chunk's place");
 static_assert(ll_lds_bytes(RBF_LL_MAX_N) <= 160 * 1024 - 256, "RBF_LL_MAX_N");
 __host__ __device__ constexpr int ll_ls(int jp, int j) { return jp * (jp - 1) / 2 + j; }  // L_D block (jp, j), jp > j
 
@@ -1584,9 +1585,9 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
   double* Ab = smem;                                   // [4096]: the A chunk, tiles [c-group][jl][64]
   double* Dg = smem + LL_OFF_DG;                       // [10][4][64]: L_D(jp, j) (6), then the inverses (4)
   double* lf = smem + LL_OFF_LF;                       // [576] the leaf; backward: [2][64] right-hand sides + [2][16]
-  double* zv = smem + LL_OFF_Z;                        // [2][n64]
+  double* zv = smem;                                   // [2][n64] (backward; the chunk's place)
   const int np = ll_np(N);
-  double* gl = zv + 2 * n64;                           // g = A u
+  double* gl = smem + LL_OFF_G;                        // g = A u
   double* cvl = gl + np;                               // c = H b
   double* mvl = cvl + np;                              // m = (HAH)[:, n]
   float* xs = reinterpret_cast<float*>(mvl + np);
@@ -1629,7 +1630,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
         const float x = lu[base + j], y = lv[base + j];
         xs[j] = x, ys[j] = y;
         xyT[(int64_t)j * P + p] = make_float2(x, y);
-        zv[j] = ldd(I + base + j);  // b (zv is free until the backward pass)
+        cvl[j] = ldd(I + base + j);  // b (c = H b is formed in place)
       } else {
         xs[j] = 0.f, ys[j] = 0.f, gl[j] = 0.0, cvl[j] = 0.0, mvl[j] = 0.0;
       }
@@ -1642,7 +1643,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
     // row's sum added up in a fixed order; otherwise RB rows per wave, every distance of a row
     bool dup = false;
     const int T64r = (N + 63) / 64, ntl = T64r * (T64r + 1) / 2;
-    if (ntl * 128 + (TH / 64) * 512 <= LL_OFF_Z) {
+    if (ntl * 128 + (TH / 64) * 512 <= LL_OFF_G) {
       double* rowp = smem;                                  // [ntl][64]
       double* colp = rowp + ntl * 64;                       // [ntl][64]
       double* rbuf = colp + ntl * 64 + wave * 512;          // [8][64] per wave
@@ -1723,11 +1724,11 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
     __syncthreads();
     CH_MARK(1);
     double ub = 0.0, ug = 0.0;
-    for (int i = t; i < N; i += TH) ub = fma(u(i), zv[i], ub), ug = fma(u(i), gl[i], ug);
+    for (int i = t; i < N; i += TH) ub = fma(u(i), cvl[i], ub), ug = fma(u(i), gl[i], ug);
     const double utb = sum_all(ub), b2 = beta * beta * sum_all(ug);
     auto hah = [&](int i, int j, double d) { return d - beta * (u(i) * gl[j] + gl[i] * u(j)) + b2 * u(i) * u(j); };
     for (int i = t; i < N; i += TH) {
-      cvl[i] = zv[i] - beta * u(i) * utb;
+      cvl[i] = cvl[i] - beta * u(i) * utb;
       mvl[i] = hah(n, i, i < n ? dist(n, i) : 0.0);
     }
     __syncthreads();
