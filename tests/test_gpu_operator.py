@@ -217,6 +217,29 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     assert ok, err
 
 
+@pytest.mark.parametrize("n", [300, 449, 641, 642])
+def test_rbf_perpixel_llt_matches_right_looking(cuda, monkeypatch, n):
+    """r06: 256 < N <= 1022 runs the left-looking matrix-core Cholesky (rbf_solve_llt; two 4-wave pixels per CU up to
+    641 lights, one 8-wave pixel per CU above); RTI_RBF_CHOL_OLD=1 keeps r05's right-looking rbf_solve_chol.  Both
+    agree with SciPy's fp64 solve (the oracle) at 1e-8 of max(|f|, 255) on the same pixels, and with each other."""
+    ys, xs = np.mgrid[0:2, 0:3]
+    rng = np.random.default_rng(1000 + n)
+    cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
+    lu, lv = o.light_dirs_for_pixels(cams, xs.ravel(), ys.ravel())
+    inten = rng.integers(0, 256, (xs.size, n)).astype(np.int32)
+    qu, qv = rng.uniform(-1, 1, 200), rng.uniform(-1, 1, 200)
+    I = torch.as_tensor(inten, device=cuda)
+    new = rti.interpolate_rbf_perpixel(I, lu, lv, qu, qv).cpu().numpy()
+    monkeypatch.setenv("RTI_RBF_CHOL_OLD", "1")
+    old = rti.interpolate_rbf_perpixel(I, lu, lv, qu, qv).cpu().numpy()
+    ref = np.stack([o.rbf_linear(lu[p], lv[p], inten[p], qu, qv) for p in range(xs.size)])
+    for got in (new, old):
+        err, ok = relight_close(got, ref, rtol=1e-8)
+        assert ok, err
+    err, ok = relight_close(new, old, rtol=1e-8)
+    assert ok, err
+
+
 @pytest.mark.parametrize("budget_slots", [0, 2])
 def test_rbf_perpixel_gp_small_workspace_budget(cuda, monkeypatch, budget_slots):
     """Above 4089 lights the Cholesky slots (≈ 4·N² bytes each) are sized from the device's free memory, not a
