@@ -134,7 +134,16 @@ def _modes_worker(rank, world, port, partition, q):
         fitter = RowTiledFitter(mine(I8, 1), lu, lv, H, chunks=chunks, partition=partition)
         got = fitter()
         s = whole.abs().amax(-1, keepdim=True).clamp_min(1.0)
-        out["u8_h16"] = fitter.h16 is not None and float(((got - whole) / s).abs().max()) < 1e-6
+        out["u8_h16"] = fitter.u8 == "h16" and float(((got - whole) / s).abs().max()) < 1e-6
+        # (3b) the int8 fixed-point fit asked for by name (r06: RowTiledFitter maps kernel="q8" like rti.fit)
+        whole = rti.fit(I8, lu, lv, kernel="q8")
+        fitter = RowTiledFitter(mine(I8, 1), lu, lv, H, chunks=chunks, partition=partition, kernel="q8")
+        out["u8_q8"] = fitter.u8 == "q8" and bool(torch.equal(fitter(), whole))
+        # (3c) an integer kernel word reaches rti_fit_shared_pm unmasked (NT_STORE is a documented pm bit)
+        kw = rti._lib.RTI_KERNEL_NT_STORE
+        whole = rti.fit(Ipm, lu, lv, stack="pixel", kernel=kw)
+        got = RowTiledFitter(mine(Ipm, 1), lu, lv, H, stack="pixel", chunks=chunks, partition=partition, kernel=kw)()
+        out["pixel_major_kernel_word"] = bool(torch.equal(got, whole))
         # (4) per-pixel camera mode: every chunk's light vectors from its GLOBAL rows (analysis.py:228)
         cams = np.stack([W / 2 + 300 * np.cos(np.linspace(0, 6, N)), H / 2 + 300 * np.sin(np.linspace(0, 6, N)),
                          np.full(N, 400.0)], -1)
