@@ -17,7 +17,7 @@ run() {  # name seconds cmd...
   return 0
 }
 for c in ${CONFIGS:-c3 c2 c4 c10 c5 c9 c6 c7 c8 c8n200}; do
-  budget=8; [ $c = c3 ] && budget=16; extra=""; case $c in c8n200|c8n400) extra="--no-cpu";; esac
+  budget=8; [ $c = c3 ] && budget=16; extra=""; case $c in c8n200) extra="--no-cpu";; esac
   run bench_$c$SUFFIX 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_$c$SUFFIX -o run -- \
       python3 bench.py --config $c --cpu-budget $budget $extra $BENCH_ARGS
 done
