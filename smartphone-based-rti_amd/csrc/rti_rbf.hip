@@ -1569,6 +1569,66 @@ static_assert(ll_lds_bytes(RBF_LL_TWO_MAX_N) + 64 <= 80 * 1024 && 2 * ll_n64(RBF
 static_assert(ll_lds_bytes(RBF_LL_MAX_N) <= 160 * 1024 - 256, "RBF_LL_MAX_N");
 __host__ __device__ constexpr int ll_ls(int jp, int j) { return jp * (jp - 1) / 2 + j; }  // L_D block (jp, j), jp > j
 
+// The 16×16 leaf of rbf_solve_llt on one wave: T (symmetric, LDS [16][17] at smem + off_t) is FACTORED lane per row in
+// registers (lane r holds row r; step c's pivot and column c of L reach every lane by readlane: the chain per step
+// is one readlane, the pivot's inverse square root and one FMA), then INVERTED lane per column by substitution (lane
+// k computes column k of L⁻¹, L's rows broadcast from LDS); L⁻¹ is written as the A operand of the sub-panel solves
+// (slab k/4, lane r + 16·(k % 4)) at smem + off_w.  Returns true for a non-positive pivot.  Out of line: its 32
+// registers are allocated apart from the kernel's 128 of accumulators (inlined, the same code spilled 840 VGPRs;
+// r06's first quad form with ds_bpermute broadcasts took ≈ 7 µs per leaf).
+__device__ __noinline__ bool rbf_ll_leaf(int off_t, int off_w) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Lm = smem + off_t;  // [16][17]: T, then L
+  double* sv = Lm + 272;      // [16]: 1 / L[r][r]
+  double* Wd = smem + off_w;  // [4][64]
+  const int lane = threadIdx.x & 63, lr = lane & 15;
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  bool bad = false;
+  {
+    double a[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a[q] = Lm[lr * 17 + q];
+    double si = 0.0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const double d = readlane64(a[c], c);
+      bad = bad || !(d > 0.0);
+      double inv = __builtin_amdgcn_rsq(d);
+      inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
+      inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
+      const double lrc = lr == c ? d * inv : a[c] * inv;  // L[r][c] (rows r >= c are used)
+      a[c] = lr >= c ? lrc : a[c];
+      si = lr == c ? inv : si;
+#pragma unroll
+      for (int q = c + 1; q < 16; ++q) a[q] = fma(-lrc, readlane64(a[c], q), a[q]);  // −= L[r][c]·L[q][c]
+    }
+    wave_sync();  // every lane has read T before L overwrites it
+    if (lane < 16) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Lm[lr * 17 + q] = a[q];
+      sv[lr] = si;
+    }
+  }
+  wave_sync();
+  double x[16];  // column k = lr of L⁻¹
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    double v = r == lr ? 1.0 : 0.0;
+#pragma unroll
+    for (int q = 0; q < r; ++q) v = fma(-Lm[r * 17 + q], x[q], v);
+    x[r] = v * sv[r];
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Wd[(lr >> 2) * 64 + r + 16 * (lr & 3)] = x[r];
+  }
+  return bad;
+}
+
 template <typename T, int TH>
 __global__ void __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(2, 2)))
 rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const T* __restrict__ I, int N, int64_t P,
@@ -1872,57 +1932,13 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
                 s = __builtin_amdgcn_mfma_f64_16x16x4f64(Dg[(ll_ls(j, k) * 4 + sl) * 64 + lane], acc[tt][k][sl], s, 0, 0, 0);
             acc[tt][j] -= s;
           }
-          // (2) the diagonal 16×16 block T: factored AND inverted by wave j in registers, four lanes per row: lane
-          // 4i + g holds T[i][4g .. 4g + 3] and the same columns of W (= I at the start).  Step c: pivot d = T[c][c] by
-          // readlane, s = d^-1/2; T[i][c] reaches the row's quad by a DPP broadcast, column c at the lane's own four
-          // columns (T[k][c], k = 4g + q) and row c of W by ds_bpermute; T[i][k] −= T[i][c]·T[k][c]·s² (c < k <= i),
-          // W[i][k] −= T[i][c]·s · W[c][k]·s (k <= c).  W's rows scaled by their s at the end give L⁻¹ (r05's lane-
-          // per-row form needed 64 VGPRs for the block and its inverse, which spilled the whole kernel; the r06 LDS
-          // form took ≈ 10 µs per leaf)
+          // (2) the diagonal 16×16 block T, on wave j: factored and inverted by rbf_ll_leaf (out of line, so its 32
+          // registers are allocated apart from the kernel's accumulators)
           if (p0 && wave == j) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) lf[lr * 17 + 4 * g + lk] = acc[0][j][g];  // lf[i][c] = T[c][i] (symmetric)
             wave_sync();
-            const int qi = lane >> 2, qg = lane & 3;  // row, column group
-            double ta[4], tw[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ta[q] = lf[qi * 17 + 4 * qg + q], tw[q] = qi == 4 * qg + q ? 1.0 : 0.0;
-            double si = 0.0;
-            bool bad = false;
-            auto bperm = [](int src_lane, double v) {
-              const uint64_t x = __double_as_longlong(v);
-              const uint32_t lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)x);
-              const uint32_t hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(x >> 32));
-              return __longlong_as_double(((uint64_t)hi << 32) | lo);
-            };
-#pragma unroll
-            for (int c = 0; c < 16; ++c) {
-              const int cq = c & 3, cg = c >> 2;
-              const double d = readlane64(ta[cq], 4 * c + cg);
-              bad = bad || !(d > 0.0);
-              double inv = __builtin_amdgcn_rsq(d);
-              inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
-              inv = fma(0.5 * inv, fma(-d * inv, inv, 1.0), inv);
-              const double lic = bperm(4 * qi + cg, ta[cq]) * inv;  // L[i][c] (rows i > c are used)
-              if (qi == c) si = inv;
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const int k = 4 * qg + q;
-                const double lkc = bperm(4 * k + cg, ta[cq]) * inv;  // L[k][c]
-                const double wck = bperm(4 * c + qg, tw[q]) * inv;   // W[c][k]·s
-                const double tu = fma(-lic, lkc, ta[q]), wu = fma(-lic, wck, tw[q]);  // branch-free: selects, no EXEC
-                ta[q] = qi > c && k > c && k <= qi ? tu : ta[q];
-                tw[q] = qi > c && k <= c ? wu : tw[q];
-              }
-              __builtin_amdgcn_sched_barrier(0);
-            }
-            // L⁻¹[i][k] = W[i][k]·s_i as the A operand of the sub-panel solves: slab k/4 (= the column group), lane
-            // i + 16·(k % 4)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int k = 4 * qg + q;
-              Dg[(6 + j) * 256 + qg * 64 + qi + 16 * q] = k <= qi ? tw[q] * si : 0.0;
-            }
+            const bool bad = rbf_ll_leaf(LL_OFF_LF, LL_OFF_DG + (6 + j) * 256);
             if (bad && lane == 0) s_bad = 1;
           }
           __syncthreads();
