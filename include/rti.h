@@ -336,34 +336,36 @@ int rti_apply_operator_f16(const uint16_t* op_hi, const uint16_t* op_lo, int Kp,
  * for every pixel: nodes x_n = (lu[p][n], lv[p][n]) and values I[p][n], PIXEL-major as
  * compute_intensities returns them; A_ij = ‖x_i − x_j‖, A w = I solved to fp64 accuracy (what
  * SciPy's LU with partial pivoting returns, to rounding: fp64 Gauss-Jordan for N <= 80, an fp32
- * Gauss-Jordan inverse + fp64 iterative refinement to 256 with an fp64 partial-pivoting fallback
- * for ill-conditioned pixels, a blocked fp64 Cholesky of the bordered system above 256),
+ * Gauss-Jordan inverse + fp64 iterative refinement to 128 with an fp64 partial-pivoting fallback
+ * for ill-conditioned pixels, and a blocked fp64 Cholesky of the bordered system above 128: (r06) left-looking
+ * on the fp64 matrix cores to N = 1022 (two pixels per CU to 641), right-looking above),
  * f(q_e) = Σ_n w_n ‖q_e − x_n‖
  * evaluated in fp64 at luv[E][2] (device).
  * out: F64 / F32 / I32 / U8, layout RTI_OUT_PIXEL_MAJOR ([p][e], the reference's
  * [y][x][ly][lx]) or RTI_OUT_EVAL_MAJOR ([e][p], prepare_images_data's [ly][lx][y][x]).
  * status: device int the caller zeroes; set to RTI_ERR_SINGULAR when a pixel's system is
  * singular (that pixel's outputs are NaN), where SciPy raises LinAlgError.  N <= 32768 (RTI_ERR_UNSUPPORTED
- * above): the Cholesky's panels narrow from 32 columns at N <= 568 to 1 at N <= 4089 (the panel in LDS), and
- * above 4089 only the 32×32 diagonal block stays in LDS while the panel is solved in place in the slot.
+ * above): above 1022 the right-looking Cholesky's panels narrow from 16 columns to 1 at N <= 4089 (the panel in
+ * LDS), and above 4089 only the 32×32 diagonal block stays in LDS while the panel is solved in place in the slot.
  * Device memory: the call allocates (stream-ordered, hipMallocAsync) and frees a workspace of
- * P·N·(8 + 8) bytes (weights + nodes) plus, for N > 256, one Cholesky slot of ≈ 4·(N+pad)² bytes (the packed
- * lower triangle) per workgroup on min(P, CUs) workgroups (≈ 3.3 GB at N = 1800, 6.7 GB at N = 2556, 17 GB at
+ * P·N·(8 + 8) bytes (weights + nodes) plus, for N > 128, one Cholesky slot of ≈ 4·(N+pad)² bytes (L as the matrix
+ * cores' 16×4 tiles plus the 64×64 diagonal blocks' factors to N = 1022, then the packed lower triangle) per
+ * workgroup on min(P, 2·CUs) workgroups to N = 641, min(P, CUs) above (≈ 0.23 GB at N = 400, 3.3 GB at N = 1800, 6.7 GB at N = 2556, 17 GB at
  * N = 4089 on 256 CUs; above 4089 as many slots as fit in min(48 GiB, 90 % of the device's free memory less the
  * weights and nodes), halved again while the allocation fails, at least one; the environment variable
- * RTI_RBF_GP_WS_BYTES lowers that budget), or for 139 <= N <= 256 an fp64
- * fallback slot of 8·N·(N+1) bytes per CU (below: in LDS),
+ * RTI_RBF_GP_WS_BYTES lowers that budget), or, for the fp32 inverses' fallback above N = 138 (reached only
+ * with the RTI_RBF_LLT_MIN_N / RTI_RBF_CHOL_OLD measurement switches), 8·N·(N+1) bytes per CU (below: in LDS),
  * plus a P + 1 int list of the fallback's pixels; RTI_ERR_HIP if it cannot. */
 int rti_rbf_perpixel(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                      const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
                      rti_stream_t stream);
 /* The same, and fallback_px (NULL, or a device int the caller zeroes) receives the number of pixels the
- * fp32-inverse solvers (81 <= N <= 256) handed to the fp64 partial-pivoting fallback (ill-conditioned:
+ * fp32-inverse solvers (81 <= N <= 128) handed to the fp64 partial-pivoting fallback (ill-conditioned:
  * nearly repeated light directions). */
 int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void* I, int in_dtype, int N, int64_t P,
                         const double* luv, int E, void* out, int out_dtype, int out_layout, int* status,
                         int* fallback_px, rti_stream_t stream);
-/* Cholesky workgroups (= workspace slots) of this thread's most recent rti_rbf_perpixel call (N > 256), 0 for
+/* Cholesky workgroups (= workspace slots) of this thread's most recent rti_rbf_perpixel call (N > 128), 0 for
  * the other solvers.  For tests and timing tools; the results do not depend on it. */
 int64_t rti_rbf_last_chol_grid(void);
 

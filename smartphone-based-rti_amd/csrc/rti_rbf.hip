@@ -2115,10 +2115,16 @@ int gji_refine() {
 }
 
 bool uses_gji(int N) { return N > RBF_GJ_MAX_N || (N >= 2 && N >= gji_min_n()); }
-// (r06) the left-looking matrix-core Cholesky for 256 < N <= RBF_LL_MAX_N; RTI_RBF_CHOL_OLD=1 (environment, read per
-// call: a measurement switch) keeps the right-looking rbf_solve_chol for A/B
+// (r06) the left-looking matrix-core Cholesky for RBF_LL_MIN_N <= N <= RBF_LL_MAX_N: in fp64 throughout it also
+// replaces the fp32 Gauss-Jordan inverses + refinement (and their fp64 fallback) above 128 lights — solve of a
+// 400² ROI 32.8 vs 64.4 ms at N = 129, 85.8 vs 104.1 at 200, 88.9 vs 413.3 at 256, while at N <= 128 the
+// register-blocked inverse stays faster (27.9 vs 32.2 ms at 128; profiles/r06k_rbf_llt_small_n_ab.log).
+// Measurement switches (environment, read per call): RTI_RBF_LLT_MIN_N moves the lower bound, RTI_RBF_CHOL_OLD=1
+// turns the left-looking form off (r05's solvers: rbf_solve_gjs / gji above 128, rbf_solve_chol above 256)
+constexpr int RBF_LL_MIN_N = 129;
 bool uses_llt(int N) {
-  if (N <= RBF_MAX_N || N > RBF_LL_MAX_N) return false;
+  const char* lo = getenv("RTI_RBF_LLT_MIN_N");
+  if (N < (lo ? atoi(lo) : RBF_LL_MIN_N) || N < 2 || N > RBF_LL_MAX_N) return false;
   const char* e = getenv("RTI_RBF_CHOL_OLD");
   return !(e && atoi(e));
 }
@@ -2130,7 +2136,7 @@ void launch_solve(const float* lu, const float* lv, const void* I, int N, int64_
                   hipStream_t s) {
   const T* In = static_cast<const T*>(I);
   const dim3 g((unsigned)P);
-  if (N > RBF_MAX_N) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
+  if (N > RBF_MAX_N || uses_llt(N)) {  // blocked fp64 Cholesky, one workgroup per CU striding over the pixels
     const unsigned cg = (unsigned)(P < chol_grid ? P : chol_grid);
     if (uses_llt(N)) {  // (r06) left-looking on the matrix cores: two 4-wave pixels per CU, or one 8-wave
       const size_t lds = ll_lds_bytes(N);
@@ -2249,7 +2255,7 @@ extern "C" int rti_rbf_perpixel_ex(const float* lu, const float* lv, const void*
   // workspace: per-pixel weights and nodes, node-major ([N][P]) for the coalesced evaluation
   void* ws = nullptr;
   // + for the block solvers: the fp64 fallback's pixel list and (N > RBF_FB_LDS_N) per-workgroup matrices
-  const bool chol = N > RBF_MAX_N, fb = !chol && uses_gji(N);
+  const bool chol = N > RBF_MAX_N || uses_llt(N), fb = !chol && uses_gji(N);
   // the Cholesky path: one workgroup (and one [ld][ld] fp64 slot) per CU, striding over the pixels
   int64_t chol_grid = chol ? (uses_llt(N) && N <= RBF_LL_TWO_MAX_N ? 2 * (int64_t)device_cus() : device_cus()) : 0;
   if (chol_grid > P) chol_grid = P;

@@ -217,11 +217,12 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     assert ok, err
 
 
-@pytest.mark.parametrize("n", [300, 449, 641, 642])
+@pytest.mark.parametrize("n", [129, 200, 256, 300, 449, 641, 642])
 def test_rbf_perpixel_llt_matches_right_looking(cuda, monkeypatch, n):
-    """r06: 256 < N <= 1022 runs the left-looking matrix-core Cholesky (rbf_solve_llt; two 4-wave pixels per CU up to
-    641 lights, one 8-wave pixel per CU above); RTI_RBF_CHOL_OLD=1 keeps r05's right-looking rbf_solve_chol.  Both
-    agree with SciPy's fp64 solve (the oracle) at 1e-8 of max(|f|, 255) on the same pixels, and with each other."""
+    """r06: 129 <= N <= 1022 runs the left-looking matrix-core Cholesky (rbf_solve_llt; two 4-wave pixels per CU up
+    to 641 lights, one 8-wave pixel per CU above); RTI_RBF_CHOL_OLD=1 keeps r05's solvers (the fp32 Gauss-Jordan
+    inverses + refinement up to 256, the right-looking rbf_solve_chol above).  Both agree with SciPy's fp64 solve
+    (the oracle) at 1e-8 of max(|f|, 255) on the same pixels, and with each other."""
     ys, xs = np.mgrid[0:2, 0:3]
     rng = np.random.default_rng(1000 + n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
@@ -300,7 +301,7 @@ def test_rbf_perpixel_near_repeated_nodes_fp64_fallback(cuda, n, d):
     qu, qv = rng.uniform(-1, 1, 200), rng.uniform(-1, 1, 200)
     stats = {}
     out = rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv, stats=stats).cpu().numpy()
-    assert stats["fallback_px"] <= 1  # only the perturbed pixel may need it (N > 256: the Cholesky, no fallback)
+    assert stats["fallback_px"] <= 1  # only the perturbed pixel may need it (N >= 129: the Cholesky, no fallback)
     for p in range(4):
         ref = o.rbf_linear(lu[p], lv[p], inten[p], qu, qv)
         err, ok = relight_close(out[p], ref, rtol=1e-7 if p == 2 else 1e-8)
@@ -308,10 +309,17 @@ def test_rbf_perpixel_near_repeated_nodes_fp64_fallback(cuda, n, d):
 
 
 @pytest.mark.parametrize("n", [100, 138, 139, 200])
-def test_rbf_perpixel_fallback_many_pixels(cuda, n):
+@pytest.mark.parametrize("solver", ["gj", "llt"])
+def test_rbf_perpixel_fallback_many_pixels(cuda, monkeypatch, n, solver):
     """Every pixel of the launch nearly repeats a light direction: (nearly) all go to the fp64 fallback,
     whose list spreads them over the grid (more pixels than workgroups: each takes several), with [A | b]
-    in LDS up to N = 138 and in a global slot above; the count comes back as stats["fallback_px"]."""
+    in LDS up to N = 138 and in a global slot above; the count comes back as stats["fallback_px"].  Since r06
+    the fp64 left-looking Cholesky solves N >= 129 without any fallback ("llt": count 0); "gj" keeps r05's fp32
+    Gauss-Jordan inverses + fallback for those N (RTI_RBF_LLT_MIN_N=257, the measurement switch)."""
+    if solver == "llt" and n < 129:
+        pytest.skip("N <= 128 is the register Gauss-Jordan inverse's range")
+    if solver == "gj":
+        monkeypatch.setenv("RTI_RBF_LLT_MIN_N", "257")
     P = 300
     rng = np.random.default_rng(n + 1)
     ys, xs = np.divmod(np.arange(P), 20)
@@ -324,7 +332,10 @@ def test_rbf_perpixel_fallback_many_pixels(cuda, n):
     out = rti.interpolate_rbf_perpixel(torch.as_tensor(inten, device=cuda), lu, lv, qu, qv, stats=stats).cpu().numpy()
     # how many pixels the fp32 inverse gives up on depends on N and the geometry (N = 100: 295 of 300, more than
     # the 256 workgroups, so some take two list entries; N = 138: 127)
-    assert (257 if n == 100 else 1) <= stats["fallback_px"] <= P
+    if solver == "llt":
+        assert stats["fallback_px"] == 0
+    else:
+        assert (257 if n == 100 else 1) <= stats["fallback_px"] <= P
     for p in list(range(0, P, 37)) + [P - 1]:
         ref = o.rbf_linear(lu[p], lv[p], inten[p], qu, qv)
         err, ok = relight_close(out[p], ref, rtol=1e-6)  # cond(A) ~ 1e9..1e10: both fp64 solves err ~ cond·eps
