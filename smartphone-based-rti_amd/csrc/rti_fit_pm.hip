@@ -636,8 +636,9 @@ fit_pm_vgen(const float* __restrict__ pinv, int N, const T* __restrict__ I, int6
 template <int K, int NS>
 constexpr int pm_direct_run() { return K > 9 ? 12 : 24; }  // groups per run (a multiple of the depth)
 
-// NTS: the bursts' stores non-temporal (RTI_KERNEL_NT_STORE; pixel-major)
-template <int K, typename T, int LAYOUT, int NS, int D, bool NTS = false>
+// NTS: the bursts' stores non-temporal (RTI_KERNEL_NT_STORE; pixel-major).  PROBE (measurement builds only,
+// tools/probe/pm_probe.hip; the C ABI cannot reach it): 1 = the bursts' global stores dropped
+template <int K, typename T, int LAYOUT, int NS, int D, bool NTS = false, int PROBE = 0>
 __global__ void __launch_bounds__(256)
 fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
               float* __restrict__ coef, int64_t ocstride, int ngrp, int nrun, int r0, int tr) {
@@ -722,6 +723,9 @@ fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int64_t px0 = (int64_t)sj * RPX;  // first pixel of the run in its channel
+    if constexpr (PROBE == 1) {  // measurement: keep the LDS parking, drop the global stores
+      if (buf[lane] == -1.2345f) coef[0] = buf[lane];
+    } else {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(coef + (int64_t)sc * ocstride, (short)0,
                                                                         (int)(P * K * 4), 0x00020000);
     if constexpr (LAYOUT == RTI_COEF_PIXEL_MAJOR) {
@@ -746,6 +750,7 @@ fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, in
                                                 0, 0);
         }
     }
+    }  // (PROBE)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the buffer is rewritten by the next run
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

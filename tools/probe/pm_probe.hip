@@ -64,3 +64,30 @@ extern "C" int pm_probe_vgen(const float* pinv, int N, const float* I, int64_t P
     default: return probe_t<1, 0>(pinv, N, I, P, coef, w, gens, s);
   }
 }
+
+// (r06) the DIRECT form at HSH-16 (k = 16, fp32 stack, pixel-major coefficients; the library's AUTO for
+// c4 pixel-major): mode 0 = exactly the library's launch, mode 1 = the same with the bursts' global stores dropped.
+// C channels of P pixels, channel stride P·N.
+template <int PROBE, int NS>
+static int probe_direct_t(const float* pinv, int N, const float* I, int64_t P, int C, float* coef, hipStream_t s) {
+  using namespace rti;
+  constexpr int K = 16, D = pm_direct_depth(NS), RPX = 16 * pm_direct_run<K, NS>();
+  const int64_t ngrp = (P + 15) / 16, nrun = (P + RPX - 1) / RPX, tr = nrun * C;
+  auto kern = fit_pm_direct<K, float, RTI_COEF_PIXEL_MAJOR, NS, D, false, PROBE>;
+  const size_t lds = (size_t)4 * RPX * K * sizeof(float);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+      hipSuccess)
+    return RTI_ERR_HIP;
+  const int64_t wgs = (tr + 3) / 4, cap = device_cus() * (int64_t)PM_DIRECT_WPC / 4;
+  const unsigned grid = (unsigned)(wgs < cap ? wgs : cap);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, pinv, N, I, P, P * N, coef, P * K, (int)ngrp, (int)nrun, 0,
+                     (int)tr);
+  return check_launch("pm_probe_direct");
+}
+
+extern "C" int pm_probe_direct(const float* pinv, int N, const float* I, int64_t P, int C, float* coef, int mode,
+                               void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (rti::pm_direct_ns(N) != 13) return RTI_ERR_UNSUPPORTED;  // the c4 shape (N = 193 .. 208)
+  return mode & 1 ? probe_direct_t<1, 13>(pinv, N, I, P, C, coef, s) : probe_direct_t<0, 13>(pinv, N, I, P, C, coef, s);
+}

@@ -107,12 +107,25 @@ def main():
         variants.append(("probe_vgen_same", lambda: pr(0)))
         variants.append(("probe_vgen_nostores", lambda: pr(1)))
         variants.append(("probe_vgen_contig_nostores", lambda: pr(3)))
+    if k == 16 and I.dtype == torch.float32 and os.path.exists(probe):
+        # tools/probe/pm_probe.hip: the library's direct form at HSH-16 with its burst stores dropped
+        import ctypes
+        plib = ctypes.CDLL(probe)
+        vp = ctypes.c_void_p
+
+        def prd(mode):
+            st = plib.pm_probe_direct(vp(pv.data_ptr()), N, vp(Ipm.data_ptr()), ctypes.c_int64(P), C,
+                                      vp(coef.data_ptr()), mode, vp(torch.cuda.current_stream(dev).cuda_stream))
+            assert st == 0, st
+        variants.append(("probe_direct_same", lambda: prd(0)))
+        variants.append(("probe_direct_nostores", lambda: prd(1)))
     agree = {}
     for name, fn in variants:
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        if name not in ("light_major_auto", "probe_vgen_nostores", "probe_vgen_contig_nostores"):
+        if name not in ("light_major_auto", "probe_vgen_nostores", "probe_vgen_contig_nostores",
+                        "probe_direct_nostores"):
             scale = ref.abs().amax(-1, keepdim=True).clamp_min(1e-30)
             agree[name] = float(((coef - ref).abs() / scale).max())
             coef.fill_(float("nan"))
