@@ -637,12 +637,13 @@ template <int K, int NS>
 constexpr int pm_direct_run() { return K > 9 ? 12 : 24; }  // groups per run (a multiple of the depth)
 
 // NTS: the bursts' stores non-temporal (RTI_KERNEL_NT_STORE; pixel-major).  PROBE (measurement builds only,
-// tools/probe/pm_probe.hip; the C ABI cannot reach it): 1 = the bursts' global stores dropped
-template <int K, typename T, int LAYOUT, int NS, int D, bool NTS = false, int PROBE = 0>
+// tools/probe/pm_probe.hip; the C ABI cannot reach it): 1 = the bursts' global stores dropped.  RUNX: groups per
+// run when non-zero (measurement builds)
+template <int K, typename T, int LAYOUT, int NS, int D, bool NTS = false, int PROBE = 0, int RUNX = 0>
 __global__ void __launch_bounds__(256)
 fit_pm_direct(const float* __restrict__ pinv, int N, const T* __restrict__ I, int64_t P, int64_t cstride,
               float* __restrict__ coef, int64_t ocstride, int ngrp, int nrun, int r0, int tr) {
-  constexpr int RUN = pm_direct_run<K, NS>(), RPX = 16 * RUN;  // groups and pixels per run
+  constexpr int RUN = RUNX ? RUNX : pm_direct_run<K, NS>(), RPX = 16 * RUN;  // groups and pixels per run
   static_assert(RUN % D == 0, "runs of whole pipeline steps");
   typedef unsigned int u4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) float runbuf[];  // per wave: RPX·K floats

@@ -66,28 +66,50 @@ extern "C" int pm_probe_vgen(const float* pinv, int N, const float* I, int64_t P
 }
 
 // (r06) the DIRECT form at HSH-16 (k = 16, fp32 stack, pixel-major coefficients; the library's AUTO for
-// c4 pixel-major): mode 0 = exactly the library's launch, mode 1 = the same with the bursts' global stores dropped.
-// C channels of P pixels, channel stride P·N.
-template <int PROBE, int NS>
-static int probe_direct_t(const float* pinv, int N, const float* I, int64_t P, int C, float* coef, hipStream_t s) {
+// c4 pixel-major): mode 0 = exactly the library's launch; bit 0: the bursts' global stores dropped; bit 2:
+// non-temporal burst stores; bit 1: "phase" launches — runs of 20 groups (the whole 160-KiB LDS at 8 waves per CU)
+// and one run per wave per launch, so every wave of a launch reads its run and then all of them store (the mix
+// probe's "stores after the sweep" placement); bit 3: the same with runs of 10 groups, two per wave
+// per launch.  C channels of P pixels, channel stride P·N.
+template <int PROBE, int NS, int RUNX, bool NTS>
+static int probe_direct_t(const float* pinv, int N, const float* I, int64_t P, int C, float* coef, int per_wave,
+                          hipStream_t s) {
   using namespace rti;
-  constexpr int K = 16, D = pm_direct_depth(NS), RPX = 16 * pm_direct_run<K, NS>();
+  constexpr int K = 16, D = pm_direct_depth(NS), RUN = RUNX ? RUNX : pm_direct_run<K, NS>(), RPX = 16 * RUN;
   const int64_t ngrp = (P + 15) / 16, nrun = (P + RPX - 1) / RPX, tr = nrun * C;
-  auto kern = fit_pm_direct<K, float, RTI_COEF_PIXEL_MAJOR, NS, D, false, PROBE>;
+  auto kern = fit_pm_direct<K, float, RTI_COEF_PIXEL_MAJOR, NS, D, NTS, PROBE, RUNX>;
   const size_t lds = (size_t)4 * RPX * K * sizeof(float);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
       hipSuccess)
     return RTI_ERR_HIP;
-  const int64_t wgs = (tr + 3) / 4, cap = device_cus() * (int64_t)PM_DIRECT_WPC / 4;
-  const unsigned grid = (unsigned)(wgs < cap ? wgs : cap);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, pinv, N, I, P, P * N, coef, P * K, (int)ngrp, (int)nrun, 0,
-                     (int)tr);
+  const int64_t cap = device_cus() * (int64_t)PM_DIRECT_WPC / 4;
+  const int64_t per = per_wave ? cap * 4 * per_wave : tr;  // runs per launch
+  for (int64_t r0 = 0; r0 < tr; r0 += per) {
+    const int64_t n = tr - r0 < per ? tr - r0 : per, wgs = (n + 3) / 4;
+    const unsigned grid = (unsigned)(wgs < cap ? wgs : cap);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, pinv, N, I, P, P * N, coef, P * K, (int)ngrp, (int)nrun,
+                       (int)r0, (int)n);
+  }
   return check_launch("pm_probe_direct");
+}
+
+template <int PROBE>
+static int probe_direct_m(const float* pinv, int N, const float* I, int64_t P, int C, float* coef, int mode,
+                          hipStream_t s) {
+  const bool nts = mode & 4;
+  if (mode & 2)
+    return nts ? probe_direct_t<PROBE, 13, 20, true>(pinv, N, I, P, C, coef, 1, s)
+               : probe_direct_t<PROBE, 13, 20, false>(pinv, N, I, P, C, coef, 1, s);
+  if (mode & 8)
+    return nts ? probe_direct_t<PROBE, 13, 10, true>(pinv, N, I, P, C, coef, 2, s)
+               : probe_direct_t<PROBE, 13, 10, false>(pinv, N, I, P, C, coef, 2, s);
+  return nts ? probe_direct_t<PROBE, 13, 0, true>(pinv, N, I, P, C, coef, 0, s)
+             : probe_direct_t<PROBE, 13, 0, false>(pinv, N, I, P, C, coef, 0, s);
 }
 
 extern "C" int pm_probe_direct(const float* pinv, int N, const float* I, int64_t P, int C, float* coef, int mode,
                                void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (rti::pm_direct_ns(N) != 13) return RTI_ERR_UNSUPPORTED;  // the c4 shape (N = 193 .. 208)
-  return mode & 1 ? probe_direct_t<1, 13>(pinv, N, I, P, C, coef, s) : probe_direct_t<0, 13>(pinv, N, I, P, C, coef, s);
+  return mode & 1 ? probe_direct_m<1>(pinv, N, I, P, C, coef, mode, s) : probe_direct_m<0>(pinv, N, I, P, C, coef, mode, s);
 }

@@ -117,15 +117,16 @@ def main():
             st = plib.pm_probe_direct(vp(pv.data_ptr()), N, vp(Ipm.data_ptr()), ctypes.c_int64(P), C,
                                       vp(coef.data_ptr()), mode, vp(torch.cuda.current_stream(dev).cuda_stream))
             assert st == 0, st
-        variants.append(("probe_direct_same", lambda: prd(0)))
-        variants.append(("probe_direct_nostores", lambda: prd(1)))
+        for name, mode in (("same", 0), ("nostores", 1), ("nts", 4), ("phase20", 2), ("phase20_nts", 6),
+                           ("phase10x2", 8), ("phase10x2_nts", 12), ("phase20_nostores", 3)):
+            variants.append((f"probe_direct_{name}", lambda mode=mode: prd(mode)))
     agree = {}
     for name, fn in variants:
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
         if name not in ("light_major_auto", "probe_vgen_nostores", "probe_vgen_contig_nostores",
-                        "probe_direct_nostores"):
+                        "probe_direct_nostores", "probe_direct_phase20_nostores"):
             scale = ref.abs().amax(-1, keepdim=True).clamp_min(1e-30)
             agree[name] = float(((coef - ref).abs() / scale).max())
             coef.fill_(float("nan"))
