@@ -1681,6 +1681,16 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
 #ifdef RTI_CHOL_PROFILE
   long long prof_[16] = {}, last_ = wall_clock64();
 #endif
+  // (r06) the row groups past n — the padding up to n64, all inside the last block column's diagonal block — are never
+  // factored as rows below an earlier block: their L rows there are zero (S is the identity on the padding), so their
+  // tiles are zeroed once per launch and afterwards only read (as the last block column's A chunk and B operands)
+  const int nrr = (n + 15) / 16;  // row groups holding real rows
+  for (int K = 0; K + 1 < nbc; ++K)
+    for (int rg = nrr; rg < G - 1; ++rg) {
+      double* tb = tile(rg, 16 * K);  // the row group's 16 tiles of block column K are consecutive
+      for (int idx = t; idx < 1024; idx += TH) tb[idx] = 0.0;
+    }
+  __syncthreads();
 
   for (int64_t p = blockIdx.x; p < P; p += gridDim.x) {
     const int64_t base = p * N;
@@ -1808,12 +1818,28 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
     // ---- the factorization, block column by block column -------------------------------------------
     for (int J = 0; J < nbc && !s_bad; ++J) {  // s_bad: block-uniform after each sync
       const int J0 = 64 * J, rgd = J0 / 16;
-      for (int rgp = rgd; rgp < G; rgp += PASS) {  // passes of up to 32 row groups
+      // the block column's row groups, as logical indices q in [rgd, Ge): q < Ge − 1 is row group q, q = Ge − 1 the
+      // right-hand-side group G − 1; before the last block column the padding groups [nrr, G − 1) are left out
+      const int Ge = J + 1 < nbc ? nrr + 1 : G;
+      // the 16-column sub-panels holding real columns (4 but in the last block column)
+      const int nsp4 = J + 1 < nbc ? 4 : (n - J0 + 15) / 16;
+      if (nsp4 < 4) {  // the padding sub-panels are skipped below: their L_D blocks are zero, their inverses I
+        for (int idx = t; idx < 2560; idx += TH) {
+          const int sl = idx >> 8, e = idx & 255, jp = sl < 6 ? (sl >= 3 ? 3 : sl >= 1 ? 2 : 1) : 0;
+          const int jj = sl < 6 ? sl - jp * (jp - 1) / 2 : sl - 6;  // slot ll_ls(jp, jj) or the inverse of jj
+          const int c = 4 * (e >> 6) + ((e & 63) >> 4), r = e & 15;
+          if (jj >= nsp4) Dg[idx] = sl >= 6 && r == c ? 1.0 : 0.0;
+        }
+      }
+      for (int rgp = rgd; rgp < Ge; rgp += PASS) {  // passes of up to PASS row groups
         const bool p0 = rgp == rgd;
         int rgt[RGW];
         bool vt[RGW];
 #pragma unroll
-        for (int tt = 0; tt < RGW; ++tt) rgt[tt] = rgp + wave + NWV * tt, vt[tt] = rgt[tt] < G;
+        for (int tt = 0; tt < RGW; ++tt) {
+          const int q = rgp + wave + NWV * tt;
+          rgt[tt] = q < Ge - 1 ? q : G - 1, vt[tt] = q < Ge;
+        }
         static_assert(NWV >= 4, "the 4 diagonal sub-blocks are the first row groups of waves 0..3");
         const bool dg = p0 && wave < 4;  // this wave's first row group is diagonal sub-block `wave`
         dx4 acc[RGW][4];
@@ -1837,9 +1863,9 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
         };
         // the row groups this wave holds in this pass are a prefix tt < ntt (wave-uniform): one branch-free K loop per
         // count, so the inner loop has no per-row-group conditions (every wave still takes every chunk's barrier)
-        const int ntt = max(0, min(RGW, (G - rgp - wave + NWV - 1) / NWV));
-        auto kloop = [&](auto ntc) {
-          constexpr int NT = decltype(ntc)::value;
+        const int ntt = max(0, min(RGW, (Ge - rgp - wave + NWV - 1) / NWV));
+        auto kloop = [&](auto ntc, auto ncgc) {
+          constexpr int NT = decltype(ntc)::value, NCG = decltype(ncgc)::value;  // NCG: column groups with real columns
           // B operands from the slot (the diagonal row groups' too: the chunk just staged left them in L2) through a
           // 4-deep ring that runs across the chunks: column group jl + 4's loads issue behind jl's MFMAs, the next
           // chunk's first four during this chunk's last four (the tiles were written block columns ago: no barrier
@@ -1864,13 +1890,13 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
               const int kn = K + 1 < J ? K + 1 : K;  // (the last chunk re-reads its own first tiles: harmless)
 #pragma unroll
               for (int jl = 0; jl < 16; ++jl) {
-                double a[4];
+                double a[NCG];
 #pragma unroll
-                for (int cg = 0; cg < 4; ++cg) a[cg] = Ak[(cg * 16 + jl) * 64 + lane];
+                for (int cg = 0; cg < NCG; ++cg) a[cg] = Ak[(cg * 16 + jl) * 64 + lane];
 #pragma unroll
                 for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
-                  for (int cg = 0; cg < 4; ++cg)
+                  for (int cg = 0; cg < NCG; ++cg)
                     acc[tt][cg] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cg], bq[jl & 3][tt], acc[tt][cg], 0, 0, 0);
 #pragma unroll
                 for (int tt = 0; tt < NT; ++tt) bq[jl & 3][tt] = jl + 4 < 16 ? bp[tt][(jl + 4) * 64] : ldb(kn, jl - 12, tt);
@@ -1881,12 +1907,24 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           }
         };
         static_assert(RGW == 4, "the K-loop dispatch below");
-        switch (ntt) {
-          case 4: kloop(std::integral_constant<int, 4>{}); break;
-          case 3: kloop(std::integral_constant<int, 3>{}); break;
-          case 2: kloop(std::integral_constant<int, 2>{}); break;
-          case 1: kloop(std::integral_constant<int, 1>{}); break;
-          default: kloop(std::integral_constant<int, 0>{}); break;
+        using I4 = std::integral_constant<int, 4>;
+        // (r06) the last block column's column groups past n are padding: their Cᵀ is zero (the A chunk's padding
+        // rows are zero tiles), so the K loop runs only the first nsp of them — for the wave counts the last block
+        // column has (its 4 diagonal row groups and the right-hand-side group: at most 2 per wave)
+        switch (nsp4 < 4 ? ntt * 8 + nsp4 : 64 + ntt) {
+          case 1 * 8 + 1: kloop(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}); break;
+          case 1 * 8 + 2: kloop(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}); break;
+          case 1 * 8 + 3: kloop(std::integral_constant<int, 1>{}, std::integral_constant<int, 3>{}); break;
+          case 2 * 8 + 1: kloop(std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}); break;
+          case 2 * 8 + 2: kloop(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}); break;
+          case 2 * 8 + 3: kloop(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{}); break;
+          case 64 + 4: case 4 * 8 + 1: case 4 * 8 + 2: case 4 * 8 + 3:
+            kloop(std::integral_constant<int, 4>{}, I4{}); break;
+          case 64 + 3: case 3 * 8 + 1: case 3 * 8 + 2: case 3 * 8 + 3:
+            kloop(std::integral_constant<int, 3>{}, I4{}); break;
+          case 64 + 2: kloop(std::integral_constant<int, 2>{}, I4{}); break;
+          case 64 + 1: kloop(std::integral_constant<int, 1>{}, I4{}); break;
+          default: kloop(std::integral_constant<int, 0>{}, I4{}); break;
         }
         CH_MARK(3);
         // C = S − Cᵀ (S from the distances, in registers)
@@ -1919,6 +1957,8 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
         // the four 16-column sub-panels
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+          if (j >= nsp4) break;  // padding sub-panels (block-uniform): acc stays S − Cᵀ = 0 for every row but the
+                                 // padding rows' own diagonal, which the diagonal area already holds as L_D = I
           // (1) update by the finished sub-panels k < j: acc[j] −= L_D(j, k) · X_k  (rows of the diagonal
           // sub-block `wave` need sub-panels j <= wave only)
 #pragma unroll
@@ -2021,7 +2061,8 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
     };
     for (int J = nbc - 1; J >= 0; --J) {
       const int J0 = 64 * J, rgd = J0 / 16;
-      if (J + 1 < nbc) gemv(J, rgd + 4, rgd + 8);  // block J + 1's rows (its z_{J+1} was solved last iteration)
+      // (rows of the padding groups are zero in L and in z: the ranges end at nrr)
+      if (J + 1 < nbc) gemv(J, rgd + 4, min(rgd + 8, nrr));  // block J + 1's rows (its z_{J+1} was solved last iteration)
 #pragma unroll
       for (int h = 0; h < CW; ++h)
 #pragma unroll
@@ -2038,7 +2079,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
       for (int idx = t; idx < LL_DIAG; idx += TH) Dg[idx] = diagw[(int64_t)J * LL_DIAG + idx];
       __syncthreads();
       CH_MARK(9);
-      if (J > 0) gemv(J - 1, rgd + 4, G - 1);  // block column J − 1's rows beyond block J: their z are final
+      if (J > 0) gemv(J - 1, rgd + 4, nrr);  // block column J − 1's rows beyond block J: their z are final
       if (wave == 0) {  // L_Dᵀ z = rhs by 16×16 blocks: lanes 0–15 the first right-hand side, 16–31 the second
         const int c = lr, rh = lk & 1;
         double* zl = zv + rh * n64 + J0;
