@@ -1852,8 +1852,10 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
         auto stage_chunk = [&](int K) {
           constexpr int SQ = 2048 / TH;  // double2 per thread
           const double2* src = reinterpret_cast<const double2*>(tile(rgd, 16 * K));
+          const int hq = nsp4 * SQ / 4;  // (the last block column: only its real row groups' tiles)
 #pragma unroll
           for (int h = 0; h < SQ; h += 4) {
+            if (h >= hq) break;
             double2 v[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = src[t + (h + q) * TH];
@@ -1943,6 +1945,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           const bool rhs = rgt[tt] == G - 1;  // wave-uniform: the right-hand-side rows n64 + lr (c₁ for lr = 0, m for 1)
 #pragma unroll
           for (int cg = 0; cg < 4; ++cg) {
+            if (cg >= nsp4) break;  // padding column groups: S and Cᵀ are zero, acc stays 0
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               const int o = 16 * cg + 4 * g;
