@@ -1642,6 +1642,8 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
   const int n = N - 1, n64 = ll_n64(N), nbc = n64 / 64, G = n64 / 16 + 1;
   double* slot = ws + (int64_t)blockIdx.x * ll_slot_doubles(N);
   double* diagw = slot + ll_col_tiles(G, nbc) * 1024;  // [nbc][LL_DIAG]
+  const __amdgpu_buffer_rsrc_t slot_rs =  // the slot's tiles, for the A chunks' LDS-DMA
+      __builtin_amdgcn_make_buffer_rsrc(slot, (short)0, (int)(ll_col_tiles(G, nbc) * 1024 * 8), 0x00020000);
   double* Ab = smem;                                   // [4096]: the A chunk, tiles [c-group][jl][64]
   double* Dg = smem + LL_OFF_DG;                       // [10][4][64]: L_D(jp, j) (6), then the inverses (4)
   double* lf = smem + LL_OFF_LF;                       // [576] the leaf; backward: [2][64] right-hand sides + [2][16]
@@ -1848,21 +1850,6 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
 #pragma unroll
           for (int cg = 0; cg < 4; ++cg) acc[tt][cg] = dx4{0.0, 0.0, 0.0, 0.0};
         // Cᵀ[c][i] = Σ_{q < J0} L[J0 + c][q]·L[i][q], one earlier block column K per LDS chunk
-        // one earlier block column K per chunk: rows J0 .. J0 + 63 of K (64 consecutive tiles, 32 KB) staged in LDS
-        auto stage_chunk = [&](int K) {
-          constexpr int SQ = 2048 / TH;  // double2 per thread
-          const double2* src = reinterpret_cast<const double2*>(tile(rgd, 16 * K));
-          const int hq = nsp4 * SQ / 4;  // (the last block column: only its real row groups' tiles)
-#pragma unroll
-          for (int h = 0; h < SQ; h += 4) {
-            if (h >= hq) break;
-            double2 v[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = src[t + (h + q) * TH];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) reinterpret_cast<double2*>(Ab)[t + (h + q) * TH] = v[q];
-          }
-        };
         // the row groups this wave holds in this pass are a prefix tt < ntt (wave-uniform): one branch-free K loop per
         // count, so the inner loop has no per-row-group conditions (every wave still takes every chunk's barrier)
         const int ntt = max(0, min(RGW, (Ge - rgp - wave + NWV - 1) / NWV));
@@ -1881,31 +1868,62 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
 #pragma unroll
                 for (int tt = 0; tt < NT; ++tt) bq[d][tt] = ldb(0, d, tt);
           }
-          for (int K = 0; K < J; ++K) {
-            const double* Ak = Ab;
-            stage_chunk(K);
-            __syncthreads();
+          // (r06) the A chunk in two 16-KB halves (column tiles 0–7 / 8–15 of its row groups), each filled by LDS-DMA one
+          // half-step ahead into the other buffer: half-step h = 2K + hf computes from Ab + 2048·(h & 1) while the DMA of
+          // h + 1 is in flight.  Per half-step: this wave's DMA(h) retired by a counted vmcnt (the 8·NT B-ring loads issued
+          // after it may stay in flight), one barrier (every wave's DMA(h) landed, every read of the other buffer done),
+          // then DMA(h + 1) and the MFMAs.  (Measured: the synchronous register-staged chunk cost up to 18 % of the solve.)
+          const int nh = 2 * J;
+          auto dma_half = [&](int h) {
+            const int K = h >> 1, hf = h & 1;
+            double* dst = Ab + (h & 1) * 2048;
+            for (int q = wave; q < 4 * nsp4; q += NWV) {  // 1 KB per instruction: row group q >> 2, part q & 3
+              const int cg = q >> 2, part = q & 3;
+              const double* src = tile(rgd + cg, 16 * K + 8 * hf) + part * 128;
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  slot_rs, (__attribute__((address_space(3))) void*)(dst + cg * 512 + part * 128), 16,
+                  (int)((src - slot) * 8) + 16 * lane, 0, 0, 0);
+            }
+          };
+          if (J > 0) {
+            dma_half(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          for (int h = 0; h < nh; ++h) {
+            const int K = h >> 1, hf = h & 1;
+            if (h > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * NT) : "memory");  // this wave's DMA(h) retired
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every ds_read of the other buffer returned
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (h + 1 < nh) dma_half(h + 1);
+            const double* Ak = Ab + (h & 1) * 2048;
             if constexpr (NT > 0) {
               const double* bp[NT];
 #pragma unroll
               for (int tt = 0; tt < NT; ++tt) bp[tt] = tile(rgt[tt], 16 * K) + lane;
               const int kn = K + 1 < J ? K + 1 : K;  // (the last chunk re-reads its own first tiles: harmless)
 #pragma unroll
-              for (int jl = 0; jl < 16; ++jl) {
+              for (int j8 = 0; j8 < 8; ++j8) {
+                const int jl = 8 * hf + j8;
                 double a[NCG];
 #pragma unroll
-                for (int cg = 0; cg < NCG; ++cg) a[cg] = Ak[(cg * 16 + jl) * 64 + lane];
+                for (int cg = 0; cg < NCG; ++cg) a[cg] = Ak[(cg * 8 + j8) * 64 + lane];
 #pragma unroll
                 for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
                   for (int cg = 0; cg < NCG; ++cg)
-                    acc[tt][cg] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cg], bq[jl & 3][tt], acc[tt][cg], 0, 0, 0);
+                    acc[tt][cg] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cg], bq[j8 & 3][tt], acc[tt][cg], 0, 0, 0);
 #pragma unroll
-                for (int tt = 0; tt < NT; ++tt) bq[jl & 3][tt] = jl + 4 < 16 ? bp[tt][(jl + 4) * 64] : ldb(kn, jl - 12, tt);
+                for (int tt = 0; tt < NT; ++tt)
+                  bq[j8 & 3][tt] = jl + 4 < 16 ? bp[tt][(jl + 4) * 64] : ldb(kn, jl - 12, tt);
                 __builtin_amdgcn_sched_barrier(0);
               }
             }
-            __syncthreads();  // the chunk is rewritten by the next K
+          }
+          if (J > 0) {  // the chunk buffers are restaged by the next pass / block column: every read returned first
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
           }
         };
         static_assert(RGW == 4, "the K-loop dispatch below");
@@ -1982,7 +2000,11 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
             for (int g = 0; g < 4; ++g) lf[lr * 17 + 4 * g + lk] = acc[0][j][g];  // lf[i][c] = T[c][i] (symmetric)
             wave_sync();
             const bool bad = rbf_ll_leaf(LL_OFF_LF, LL_OFF_DG + (6 + j) * 256);
+#ifndef RTI_LLT_NOSTAGE
             if (bad && lane == 0) s_bad = 1;
+#else
+            (void)bad;
+#endif
           }
           __syncthreads();
           CH_MARK(5);
