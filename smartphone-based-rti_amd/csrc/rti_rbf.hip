@@ -1808,15 +1808,10 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
     // element (i, j) of the padded matrix [S | I_pad; c₁ᵀ; mᵀ] (row i, column j < n64), branch-free: for i, j < n,
     // −hah(i, j, d) = β·e·(g_i + g_j) − d − b2·e² (u = e on both); the right-hand-side rows are their own row group
     const double be = beta * e, b2e2 = b2 * e * e;
-    // (the column index enters as j = J0 + lk + o with o = 16·cg + 4·g a compile-time offset: the per-element tests
-    // are one compare against that immediate and one against a scalar, and the loads share one base — r06: with j
-    // itself per element the compiler kept 16 column indices per lane, spilled them, and waited on a scratch reload
-    // for every element)
-    auto s_mat = [&](bool iv, int di, int jrem, int o, const float* xj, const float* yj, const double* gj, double xi,
-                     double yi, double gi) -> double {  // di = i − J0 − lk; jrem = n − J0 − lk (j < n ⟺ o < jrem)
-      const double s = fma(be, gi + gj[o], -dist64_pos(xi, yi, (double)xj[o], (double)yj[o]) - b2e2);
-      return iv ? (o < jrem ? s : 0.0) : (di == o ? 1.0 : 0.0);
-    };
+    // (the column index enters as o = 16·cg + 4·g, a compile-time offset from J0 + lk: the per-element tests are one
+    // compare against that immediate and one against a lane value, and the loads share one base — r06: with the column
+    // index itself per element the compiler kept 16 column indices per lane, spilled them, and waited on a scratch
+    // reload for every element)
     // ---- the factorization, block column by block column -------------------------------------------
     for (int J = 0; J < nbc && !s_bad; ++J) {  // s_bad: block-uniform after each sync
       const int J0 = 64 * J, rgd = J0 / 16;
@@ -1947,29 +1942,50 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           default: kloop(std::integral_constant<int, 0>{}, I4{}); break;
         }
         CH_MARK(3);
-        // C = S − Cᵀ (S from the distances, in registers)
+        // C = S − Cᵀ (S from the distances, in registers).  (r06) Column-group outer: a column group's 4 node columns
+        // (x, y, g of node J0 + lk + 16·cg + 4·g) are read from LDS once and serve every row group of the wave, whose
+        // rows' x, y, g were read once before the loop
+        {
+          double xi[RGW], yi[RGW], gi[RGW];
+          int di[RGW];  // i − J0 − lk: the padding rows' identity entry sits at o = di
+          bool iv[RGW];
 #pragma unroll
-        for (int tt = 0; tt < RGW; ++tt) {
-          if (!vt[tt]) continue;
-          const int i = 16 * rgt[tt] + lr, ic = i < np ? i : 0;
-          const double xi = (double)xs[ic], yi = (double)ys[ic], gi = gl[ic];
-          const bool iv = i < n;
-          const int di = i - J0 - lk, jrem = n - J0 - lk;
+          for (int tt = 0; tt < RGW; ++tt) {
+            const int i = 16 * rgt[tt] + lr, ic = vt[tt] && i < np ? i : 0;
+            xi[tt] = (double)xs[ic], yi[tt] = (double)ys[ic], gi[tt] = gl[ic];
+            iv[tt] = i < n, di[tt] = i - J0 - lk;
+          }
+          const int jrem = n - J0 - lk;
           const float* xj = xs + J0 + lk;
           const float* yj = ys + J0 + lk;
           const double* gj = gl + J0 + lk;
           const double* cj = cvl + J0 + lk;
           const double* mj = mvl + J0 + lk;
-          const bool rhs = rgt[tt] == G - 1;  // wave-uniform: the right-hand-side rows n64 + lr (c₁ for lr = 0, m for 1)
 #pragma unroll
           for (int cg = 0; cg < 4; ++cg) {
             if (cg >= nsp4) break;  // padding column groups: S and Cᵀ are zero, acc stays 0
+            double xc[4], yc[4], gc[4];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               const int o = 16 * cg + 4 * g;
-              const double v = rhs ? (lr < 2 && o < jrem ? (lr == 0 ? cj[o] : mj[o]) : 0.0)
-                                   : s_mat(iv, di, jrem, o, xj, yj, gj, xi, yi, gi);
-              acc[tt][cg][g] = v - acc[tt][cg][g];
+              xc[g] = (double)xj[o], yc[g] = (double)yj[o], gc[g] = gj[o];
+            }
+#pragma unroll
+            for (int tt = 0; tt < RGW; ++tt) {
+              if (!vt[tt]) continue;
+              const bool rhs = rgt[tt] == G - 1;  // wave-uniform: the right-hand-side rows n64 + lr (c₁ for lr = 0, m for 1)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                const int o = 16 * cg + 4 * g;
+                double v;
+                if (rhs) {
+                  v = lr < 2 && o < jrem ? (lr == 0 ? cj[o] : mj[o]) : 0.0;
+                } else {
+                  const double sv = fma(be, gi[tt] + gc[g], -dist64_pos(xi[tt], yi[tt], xc[g], yc[g]) - b2e2);
+                  v = iv[tt] ? (o < jrem ? sv : 0.0) : (di[tt] == o ? 1.0 : 0.0);
+                }
+                acc[tt][cg][g] = v - acc[tt][cg][g];
+              }
             }
             __builtin_amdgcn_sched_barrier(0);  // (else every distance's operands are hoisted: spills)
           }
