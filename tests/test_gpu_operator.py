@@ -217,7 +217,7 @@ def test_rbf_perpixel_sizes_vs_oracle(cuda, n):
     assert ok, err
 
 
-@pytest.mark.parametrize("n", [129, 130, 146, 177, 193, 194, 200, 256, 300, 449, 641, 642, 660, 706])
+@pytest.mark.parametrize("n", [129, 130, 146, 177, 193, 194, 200, 256, 300, 449, 641, 642, 660, 706, 1000])
 def test_rbf_perpixel_llt_matches_right_looking(cuda, monkeypatch, n):
     """r06: 129 <= N <= 1022 runs the left-looking matrix-core Cholesky (rbf_solve_llt; two 4-wave pixels per CU up
     to 641 lights, one 8-wave pixel per CU above); RTI_RBF_CHOL_OLD=1 keeps r05's solvers (the fp32 Gauss-Jordan
@@ -225,7 +225,7 @@ def test_rbf_perpixel_llt_matches_right_looking(cuda, monkeypatch, n):
     (the oracle) at 1e-8 of max(|f|, 255) on the same pixels, and with each other.  The padding trim's cases
     (n = N − 1 padded to a multiple of 64): one real column in the last block column and three padding row groups
     (130, 194), two / three real sub-panels (146, 177), no padding (129, 193, 449, 641), and the 8-wave form with
-    padding row groups and two real sub-panels (660) or none and four (706)."""
+    padding row groups and two real sub-panels (660), three and one real column (706), one and three (1000)."""
     ys, xs = np.mgrid[0:2, 0:3]
     rng = np.random.default_rng(1000 + n)
     cams = np.stack([rng.uniform(-100, 100, n), rng.uniform(-100, 100, n), rng.uniform(60, 150, n)], -1)
