@@ -1894,6 +1894,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
             if (h + 1 < nh) dma_half(h + 1);
             const double* Ak = Ab + (h & 1) * 2048;
             if constexpr (NT > 0) {
+              __builtin_amdgcn_s_setprio(1);  // (the MFMA stream ahead of the other pixel's VALU phases on this SIMD)
               const double* bp[NT];
 #pragma unroll
               for (int tt = 0; tt < NT; ++tt) bp[tt] = tile(rgt[tt], 16 * K) + lane;
@@ -1914,6 +1915,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
                   bq[j8 & 3][tt] = jl + 4 < 16 ? bp[tt][(jl + 4) * 64] : ldb(kn, jl - 12, tt);
                 __builtin_amdgcn_sched_barrier(0);
               }
+              __builtin_amdgcn_s_setprio(0);
             }
           }
           if (J > 0) {  // the chunk buffers are restaged by the next pass / block column: every read returned first
