@@ -2014,10 +2014,12 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           // (2) the diagonal 16×16 block T, on wave j: factored and inverted by rbf_ll_leaf (out of line, so its 32
           // registers are allocated apart from the kernel's accumulators)
           if (p0 && wave == j) {
+            __builtin_amdgcn_s_setprio(2);  // the serial leaf is every wave's critical path: ahead of the other pixel
 #pragma unroll
             for (int g = 0; g < 4; ++g) lf[lr * 17 + 4 * g + lk] = acc[0][j][g];  // lf[i][c] = T[c][i] (symmetric)
             wave_sync();
             const bool bad = rbf_ll_leaf(LL_OFF_LF, LL_OFF_DG + (6 + j) * 256);
+            __builtin_amdgcn_s_setprio(0);
 #ifndef RTI_LLT_NOSTAGE
             if (bad && lane == 0) s_bad = 1;
 #else
@@ -2124,6 +2126,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
       CH_MARK(9);
       if (J > 0) gemv(J - 1, rgd + 4, nrr);  // block column J − 1's rows beyond block J: their z are final
       if (wave == 0) {  // L_Dᵀ z = rhs by 16×16 blocks: lanes 0–15 the first right-hand side, 16–31 the second
+        __builtin_amdgcn_s_setprio(2);  // (the serial solve ahead of the GEMV loads and the other pixel)
         const int c = lr, rh = lk & 1;
         double* zl = zv + rh * n64 + J0;
         // (loops kept rolled: unrolled, the compiler hoisted all 96 LDS operands and spilled the whole kernel)
@@ -2153,6 +2156,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           if (lane < 32) zl[16 * j + c] = z;
           wave_sync();
         }
+        __builtin_amdgcn_s_setprio(0);
       }
       __syncthreads();
       CH_MARK(10);
