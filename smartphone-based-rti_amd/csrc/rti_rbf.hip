@@ -1993,7 +1993,8 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           }
         }
         CH_MARK(4);
-        // the four 16-column sub-panels
+        // the four 16-column sub-panels (a barrier-bound chain: at wave priority 1, the leaves at 2)
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (j >= nsp4) break;  // padding sub-panels (block-uniform): acc stays S − Cᵀ = 0 for every row but the
@@ -2019,7 +2020,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
             for (int g = 0; g < 4; ++g) lf[lr * 17 + 4 * g + lk] = acc[0][j][g];  // lf[i][c] = T[c][i] (symmetric)
             wave_sync();
             const bool bad = rbf_ll_leaf(LL_OFF_LF, LL_OFF_DG + (6 + j) * 256);
-            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(1);
 #ifndef RTI_LLT_NOSTAGE
             if (bad && lane == 0) s_bad = 1;
 #else
@@ -2045,6 +2046,7 @@ rbf_solve_llt(const float* __restrict__ lu, const float* __restrict__ lv, const 
           __syncthreads();
           CH_MARK(6);
         }
+        __builtin_amdgcn_s_setprio(0);
         // L's tiles of this block column (the diagonal sub-blocks go to the slot's diagonal area below)
 #pragma unroll
         for (int tt = 0; tt < RGW; ++tt) {
